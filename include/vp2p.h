@@ -1,0 +1,157 @@
+/*
+ * vp2p.h — C ABI of libvp2p_hip.so, the MI355X (gfx950) kernels of Video-P2P's controlled-attention
+ * path.  Plain pointers, sizes and strides only; no torch types.  Every entry point:
+ *   - takes caller-allocated DEVICE pointers and a hipStream_t (passed as void*, 0 = null stream),
+ *   - never allocates, frees or synchronises (safe inside hipGraph capture),
+ *   - returns VP2P_OK (0) or a negative VP2P_E_* status for an unsupported shape/dtype/argument,
+ *     checked on the host BEFORE anything is launched.
+ * Strides are in ELEMENTS; the channel dimension of every activation is contiguous (stride 1) and a
+ * head's channels are [head*head_dim, (head+1)*head_dim).
+ *
+ * Which reference interface each entry point replaces (paths relative to emilycai99/Video-P2P):
+ *   vp2p_frame_attn_fwd       FrameAttention core: tuneavideo/models/attention.py:282-322
+ *                              (first-frame K/V gather :296-302 + xformers/_attention :314-322)
+ *   vp2p_cross_attn_p2p_fwd   hooked attn2 forward after the projections: ptp_utils.py:206-220,
+ *                              with the controller call :218 -> run_videop2p.py:212-224, 255-259,
+ *                              304-317, 333-363 fused into the softmax epilogue, and the
+ *                              AttentionStore sum that LocalBlend reads (:261-268, :145-146)
+ *   vp2p_temporal_attn_p2p_fwd hooked attn_temp forward (attention.py:262-268 -> ptp_utils.py:206-220)
+ *                              with replace_self_attention (run_videop2p.py:293-298, 306, 315)
+ *   vp2p_cross_kv_prep        layout pass for vp2p_cross_attn_p2p_fwd's 77-token K/V (no reference
+ *                              counterpart: the reference repeats the context per frame,
+ *                              attention.py:95)
+ *   vp2p_step_fused           CFG + DDIM step + LocalBlend: pipeline_tuneavideo.py:409-424 ->
+ *                              dependent_ddim.py:268-309 (eta = 0) -> run_videop2p.py:142-155;
+ *                              also NullInversion.next_step/prev_step (run_videop2p.py:445-463)
+ */
+#ifndef VP2P_H
+#define VP2P_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VP2P_ABI_VERSION 1
+
+enum vp2p_status {
+  VP2P_OK = 0,
+  VP2P_E_ARG = -1,        /* null pointer / negative size / inconsistent sizes */
+  VP2P_E_DTYPE = -2,      /* dtype not supported by this entry point */
+  VP2P_E_HEAD_DIM = -3,   /* head_dim without a compiled kernel instance */
+  VP2P_E_SHAPE = -4,      /* size above a kernel limit (frames > 32 temporal, tokens_kv > 128 cross) */
+  VP2P_E_LAUNCH = -5      /* hipLaunchKernelGGL reported an error */
+};
+
+enum vp2p_dtype { VP2P_F32 = 0, VP2P_BF16 = 1 };
+
+enum vp2p_edit_mode { VP2P_EDIT_NONE = 0, VP2P_EDIT_REPLACE = 1, VP2P_EDIT_REFINE = 2 };
+
+/* ---- K1: FrameAttention (first-frame K/V), flash-style, MFMA -------------------------------- */
+typedef struct vp2p_frame_attn_args {
+  const void* q;            /* (batch, frames, tokens_q, heads*head_dim) strided */
+  const void* k;            /* frame-0 keys   (batch, tokens_kv, heads*head_dim) strided */
+  const void* v;            /* frame-0 values (batch, tokens_kv, heads*head_dim) strided */
+  void* o;                  /* (batch, frames, tokens_q, heads*head_dim) strided */
+  int64_t q_sb, q_sf, q_sn;
+  int64_t k_sb, k_sn;
+  int64_t v_sb, v_sn;
+  int64_t o_sb, o_sf, o_sn;
+  int32_t batch, frames, tokens_q, tokens_kv, heads, head_dim;
+  float scale;              /* softmax scale (head_dim ** -0.5 in the reference) */
+  int32_t dtype;            /* vp2p_dtype of q/k/v/o */
+} vp2p_frame_attn_args;
+
+int vp2p_frame_attn_fwd(const vp2p_frame_attn_args* args, void* stream);
+
+/* ---- K2: hooked cross-attention (<= 128 context tokens) + fused P2P edit --------------------- */
+typedef struct vp2p_cross_attn_args {
+  const void* q;            /* (batch, frames, tokens_q, heads*head_dim) strided */
+  const void* kv_ws;        /* workspace written by vp2p_cross_kv_prep for this context */
+  void* o;                  /* (batch, frames, tokens_q, heads*head_dim) strided */
+  int64_t q_sb, q_sf, q_sn;
+  int64_t o_sb, o_sf, o_sn;
+  int32_t batch, frames, tokens_q, tokens_kv, heads, head_dim;
+  float scale;
+  int32_t dtype;
+  /* P2P.  batch = 2 * prompts: rows [0, prompts) are the unconditional half, rows
+   * [prompts, 2*prompts) the conditional half whose first prompt is the edit source. */
+  int32_t prompts;
+  int32_t edit_mode;        /* vp2p_edit_mode; applied to conditional rows of prompts 1.. */
+  int32_t reweight;         /* multiply by equalizer inside the edit (AttentionReweight) */
+  const float* alpha_words; /* (prompts-1, 77) cross_replace_alpha[cur_step] */
+  const int32_t* map_ptr;   /* REPLACE: CSC column pointers (prompts-1, tokens_kv+1) */
+  const int32_t* map_idx;   /* REPLACE: source word of each nonzero; REFINE: (prompts-1, tokens_kv) gather index */
+  const float* map_val;     /* REPLACE: value of each nonzero */
+  const float* refine_alpha;/* REFINE: (prompts-1, tokens_kv) */
+  const float* equalizer;   /* (tokens_kv) */
+  /* AttentionStore sum consumed by LocalBlend: lb_acc[p][frame][token] += sum over heads and words
+   * of lb_word_alpha[p][w] * post-edit prob (conditional rows only).  NULL = off. */
+  float* lb_acc;            /* (prompts, frames, tokens_q) fp32 */
+  const float* lb_word_alpha; /* (prompts, tokens_kv) */
+  /* Optional post-edit probabilities in the reference's attn layout
+   * ((batch*frames*heads), tokens_q, tokens_kv) fp32.  NULL = off. */
+  float* probs_out;
+} vp2p_cross_attn_args;
+
+/* Bytes of the K/V workspace for one context of the given shape (<0: unsupported). */
+int64_t vp2p_cross_kv_workspace_bytes(int32_t batch, int32_t tokens_kv, int32_t heads,
+                                      int32_t head_dim, int32_t dtype);
+
+/* Pads / transposes the projected context K, V ((batch, tokens_kv, heads*head_dim) strided) into
+ * the MFMA fragment layout vp2p_cross_attn_p2p_fwd reads (one pass over B*77*C elements). */
+int vp2p_cross_kv_prep(const void* k, const void* v, int64_t k_sb, int64_t k_sn, int64_t v_sb,
+                       int64_t v_sn, int32_t batch, int32_t tokens_kv, int32_t heads,
+                       int32_t head_dim, int32_t dtype, void* kv_ws, void* stream);
+
+int vp2p_cross_attn_p2p_fwd(const vp2p_cross_attn_args* args, void* stream);
+
+/* ---- K3: hooked temporal attention (frames <= 32) + self-attention replace -------------------- */
+typedef struct vp2p_temporal_attn_args {
+  const void* q; const void* k; const void* v; void* o;   /* (batch, frames, tokens, C) strided */
+  int64_t q_sb, q_sf, q_sn;
+  int64_t k_sb, k_sf, k_sn;
+  int64_t v_sb, v_sf, v_sn;
+  int64_t o_sb, o_sf, o_sn;
+  int32_t batch, frames, tokens, heads, head_dim;
+  float scale;
+  int32_t dtype;
+  int32_t prompts;          /* batch = 2*prompts when self_replace is set */
+  int32_t self_replace;     /* conditional rows of prompts 1.. use the source prompt's probs */
+  float* probs_out;         /* ((batch*tokens*heads), frames, frames) fp32 in '(b d)' order, or NULL */
+} vp2p_temporal_attn_args;
+
+int vp2p_temporal_attn_p2p_fwd(const vp2p_temporal_attn_args* args, void* stream);
+
+/* ---- K5+K6: classifier-free guidance + DDIM update + LocalBlend, one launch --------------------
+ *   e_p   = cfg ? u_p + g*(t_p - u_p) : n_p        (fast: e_0 = t_0)
+ *   x'_p  = c4 * ((x_p - c1*e_p) / c2) + c3*e_p    (each op rounded separately, as torch does)
+ *   blend : x''_p = x'_0 + m_p*(x'_p - x'_0), m_p = mask_0 | mask_p,
+ *           mask_p = up(pool3x3(lb_acc_p / lb_count)) / max(...) > th                           */
+typedef struct vp2p_step_args {
+  const void* noise;        /* (cfg ? 2*prompts : prompts, channels, frames, height, width) contiguous */
+  int32_t noise_dtype;
+  const float* latents;     /* (prompts, channels, frames, height, width) contiguous fp32 */
+  float* out;               /* same shape; may alias latents */
+  int32_t prompts, channels, frames, height, width;
+  int32_t cfg, fast;
+  float guidance;
+  float c1, c2, c3, c4;
+  const float* lb_acc;      /* (prompts, frames, lb_h*lb_w) or NULL = no blend */
+  int32_t lb_h, lb_w;
+  float lb_count;           /* number of maps summed per step (layers*heads): the reference's mean */
+  float lb_th;
+} vp2p_step_args;
+
+int vp2p_step_fused(const vp2p_step_args* args, void* stream);
+
+/* ---- introspection ---------------------------------------------------------------------------- */
+int vp2p_abi_version(void);
+/* Head dims with compiled kernel instances, written to out[0..n); returns the count. */
+int vp2p_supported_head_dims(int32_t* out, int32_t capacity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VP2P_H */

@@ -1,0 +1,66 @@
+"""CPU checks of the C-ABI boundary: the library loads, exports every symbol include/vp2p.h declares,
+and the ctypes structs have the C layout (sizeof/offsetof compiled from the header with gcc)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vp2p.h")
+LIB = os.path.join(ROOT, "video-p2p_amd", "lib", "libvp2p_hip.so")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t)\s+(vp2p_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_exports():
+    from vp2p import _lib
+    assert sorted(_lib.EXPORTS) == _declared()
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built (run __graft_entry__.build())")
+def test_library_exports_every_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [s for s in _declared() if s not in syms]
+    assert not missing, missing
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_library_loads_and_reports_abi():
+    from vp2p import _lib
+    lib = _lib.load()
+    assert lib.vp2p_abi_version() == _lib.ABI_VERSION
+    assert 40 in _lib.supported_head_dims() and 160 in _lib.supported_head_dims()
+    # host-side validation only (no kernel launch): bad arguments are rejected before any launch
+    assert lib.vp2p_cross_kv_workspace_bytes(4, 77, 8, 40, 1) > 0
+    assert lib.vp2p_cross_kv_workspace_bytes(4, 200, 8, 40, 1) == -4
+    assert lib.vp2p_cross_kv_workspace_bytes(4, 77, 8, 41, 1) == -3
+    assert lib.vp2p_frame_attn_fwd(None, None) == -1
+    assert lib.vp2p_temporal_attn_p2p_fwd(None, None) == -1
+
+
+def test_struct_layout_matches_header(tmp_path):
+    from vp2p import _lib
+    structs = {"vp2p_frame_attn_args": _lib.FrameAttnArgs, "vp2p_cross_attn_args": _lib.CrossAttnArgs,
+               "vp2p_temporal_attn_args": _lib.TemporalAttnArgs, "vp2p_step_args": _lib.StepArgs}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0;}")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", str(c), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    for line in filter(None, got):
+        cname, field, val = line.split()
+        py = structs[cname]
+        want = ctypes.sizeof(py) if field == "size" else getattr(py, field).offset
+        assert int(val) == want, (cname, field, val, want)

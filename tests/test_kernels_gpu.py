@@ -1,0 +1,220 @@
+"""Kernel parity on the MI355X: every HIP kernel vs the CPU oracle on the same inputs.
+
+Tolerances (BASELINE.json north_star): fp32 <= 1e-4 relative, bf16 <= 2e-2 relative (measured
+as max|err| / max|ref|).  The reference's hooked softmax uses one global max (ptp_utils.py:217);
+the kernels use a per-row max, equal wherever the reference does not underflow -- each test
+asserts the oracle output is finite (no underflowed rows) before comparing.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import p2p_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2}
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _rand(shape, seed, scale=1.0, dtype=torch.float32):
+    g = np.random.default_rng(seed)
+    x = torch.from_numpy((g.standard_normal(shape) * scale).astype(np.float32)).to(dtype)
+    return x  # CPU; values already rounded to dtype
+
+
+def _np(t):
+    return t.float().cpu().numpy()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from vp2p import _lib
+    _lib.load()
+    assert torch.cuda.is_available()
+
+
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("d,frames,n", [(40, 3, 200), (80, 2, 256), (160, 2, 144), (40, 8, 64)])
+def test_frame_attention(dtype, d, frames, n):
+    from vp2p import ops
+    heads, B = 8, 2
+    C = heads * d
+    q = _rand((B * frames, n, C), 1, 1.0, dtype)
+    k = _rand((B * frames, n, C), 2, 1.0, dtype)
+    v = _rand((B * frames, n, C), 3, 1.0, dtype)
+    ref = O.frame_attention(_np(q), _np(k), _np(v), frames, heads)
+    out = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads)
+    torch.cuda.synchronize()
+    assert _rel(_np(out), ref) < TOL[dtype], _rel(_np(out), ref)
+    # frame-0-only K/V (the production call) must give the identical result
+    k0 = k.reshape(B, frames, n, C)[:, 0].contiguous().to(DEV)
+    v0 = v.reshape(B, frames, n, C)[:, 0].contiguous().to(DEV)
+    out0 = ops.frame_attention(q.to(DEV), k0, v0, frames, heads)
+    torch.cuda.synchronize()
+    assert torch.equal(out0, out)
+
+
+def test_frame_attention_large_logits():
+    """Force the online-softmax rescale branch: a spike key late in the sequence (rule 26)."""
+    from vp2p import ops
+    heads, B, frames, n, d = 8, 1, 2, 512, 40
+    C = heads * d
+    q = _rand((B * frames, n, C), 4, 1.0)
+    k = _rand((B * frames, n, C), 5, 1.0)
+    k[0, 450] *= 12.0
+    v = _rand((B * frames, n, C), 6, 1.0)
+    ref = O.frame_attention(_np(q), _np(k), _np(v), frames, heads)
+    out = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads)
+    torch.cuda.synchronize()
+    assert _rel(_np(out), ref) < 1e-4
+
+
+# ------------------------------------------------------------------------------------------------
+def _controller(tokenizer, name, step):
+    import spec
+    prompts, swap, blend, eq, cross, self_ = spec.CONFIGS[name]
+    ctrl = O.EditController(prompts, swap, {"default_": cross}, self_, tokenizer,
+                            blend_words=None if blend is None else ((blend[0],), (blend[1],)),
+                            eq_params=eq)
+    ctrl.cur_step = step
+    return ctrl
+
+
+def _plan(ctrl, lb_alpha=None):
+    from vp2p import _lib, ops
+    mode = _lib.EDIT_REPLACE if ctrl.is_replace else _lib.EDIT_REFINE
+    return ops.CrossEditPlan(
+        ctrl.batch_size, mode, ctrl.equalizer is not None, torch.from_numpy(ctrl.cross_replace_alpha),
+        mapper=ctrl.mapper, refine_alpha=None if ctrl.is_replace else ctrl.alphas.reshape(ctrl.batch_size - 1, -1),
+        equalizer=ctrl.equalizer, lb_word_alpha=lb_alpha)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("name,step", [("rabbit", 0), ("rabbit", 12), ("car", 3), ("man", 5), ("bird", 30)])
+def test_cross_attention_p2p(tokenizer, dtype, name, step):
+    from vp2p import ops
+    heads, P, frames, n, d = 8, 2, 2, 256, 40
+    B, C = 2 * P, heads * d
+    ctrl = _controller(tokenizer, name, step)
+    lb_alpha = ctrl.local_blend.alpha_layers.reshape(P, 77) if ctrl.local_blend else np.ones((P, 77), np.float32)
+    q = _rand((B * frames, n, C), 7, 1.0, dtype)
+    k = _rand((B, 77, C), 8, 1.0, dtype)
+    v = _rand((B, 77, C), 9, 1.0, dtype)
+    kf = np.repeat(_np(k), frames, axis=0)   # context repeated per frame (attention.py:95)
+    vf = np.repeat(_np(v), frames, axis=0)
+    ref_out, ref_p = O.controlled_core(_np(q), kf, vf, heads, True, ctrl, "up")
+    assert np.isfinite(ref_p).all() and np.isfinite(ref_out).all()
+    plan = _plan(ctrl, lb_alpha)
+    lb_acc = torch.zeros(P, frames, n, device=DEV)
+    probs = torch.empty(B * frames * heads, n, 77, device=DEV)
+    out = ops.cross_attention_p2p(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, plan=plan, step=step,
+                                  lb_acc=lb_acc, probs_out=probs)
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert _rel(probs.cpu().numpy(), ref_p) < tol, _rel(probs.cpu().numpy(), ref_p)
+    assert _rel(_np(out), ref_out) < tol, _rel(_np(out), ref_out)
+    cond = ref_p.reshape(B, frames, heads, n, 77)[P:]
+    ref_lb = np.einsum("pfhnw,pw->pfn", cond, lb_alpha)
+    assert _rel(lb_acc.cpu().numpy(), ref_lb) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cross_attention_plain(dtype):
+    """No controller: plain hooked softmax-attention (DummyController, ptp_utils.py:225-234)."""
+    from vp2p import ops
+    heads, frames, n, d, B = 8, 3, 100, 80, 3
+    C = heads * d
+    q = _rand((B * frames, n, C), 10, 1.0, dtype)
+    k = _rand((B, 77, C), 11, 1.0, dtype)
+    v = _rand((B, 77, C), 12, 1.0, dtype)
+    ref, _ = O.controlled_core(_np(q), np.repeat(_np(k), frames, 0), np.repeat(_np(v), frames, 0),
+                               heads, True, None)
+    out = ops.cross_attention_p2p(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads)
+    torch.cuda.synchronize()
+    assert _rel(_np(out), ref) < TOL[dtype]
+
+
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("frames,d,step", [(8, 40, 0), (8, 40, 30), (24, 80, 3), (3, 160, 1), (16, 40, 0)])
+def test_temporal_attention_p2p(tokenizer, dtype, frames, d, step):
+    from vp2p import ops
+    heads, P, n = 8, 2, 48
+    B, C = 2 * P, heads * d
+    ctrl = _controller(tokenizer, "rabbit", step)
+    # '(b f) n c' inputs; the oracle consumes the reference's '(b d) f c' rearrangement
+    q = _rand((B * frames, n, C), 13, 1.0, dtype)
+    k = _rand((B * frames, n, C), 14, 1.0, dtype)
+    v = _rand((B * frames, n, C), 15, 1.0, dtype)
+    to_bd = lambda t: _np(t).reshape(B, frames, n, C).transpose(0, 2, 1, 3).reshape(B * n, frames, C)  # noqa
+    ref_out, ref_p = O.controlled_core(to_bd(q), to_bd(k), to_bd(v), heads, False, ctrl, "down")
+    assert np.isfinite(ref_out).all()
+    replace = ctrl.num_self_replace[0] <= step < ctrl.num_self_replace[1]
+    probs = torch.empty(B * n * heads, frames, frames, device=DEV)
+    out = ops.temporal_attention_p2p(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, prompts=P,
+                                     self_replace=replace, probs_out=probs)
+    torch.cuda.synchronize()
+    got = _np(out).reshape(B, frames, n, C).transpose(0, 2, 1, 3).reshape(B * n, frames, C)
+    assert _rel(probs.cpu().numpy(), ref_p) < TOL[dtype]
+    assert _rel(got, ref_out) < TOL[dtype], _rel(got, ref_out)
+    # the reference '(b d)' layout through the strided entry point gives the same numbers
+    bd = lambda t: torch.from_numpy(to_bd(t)).to(dtype).to(DEV)  # noqa
+    out_bd = ops.temporal_attention_p2p_bd(bd(q), bd(k), bd(v), B, heads, prompts=P, self_replace=replace)
+    torch.cuda.synchronize()
+    assert torch.equal(out_bd.cpu().float(), torch.from_numpy(got))
+
+
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("t,fast,blend", [(981, True, True), (501, False, True), (21, True, False)])
+def test_step_fused(t, fast, blend):
+    from vp2p import ops
+    P, C, F, H, W = 2, 4, 3, 64, 64
+    g = np.random.default_rng(20 + t)
+    noise = g.standard_normal((2 * P, C, F, H, W)).astype(np.float32)
+    lat = g.standard_normal((P, C, F, H, W)).astype(np.float32)
+    acc = np.abs(g.standard_normal((P, F, 256))).astype(np.float32) * 5
+    d = O.DDIM()
+    d.set_timesteps(50)
+    eps = O.cfg(noise, 7.5, fast)
+    prev = d.step(eps, t, lat)
+    if blend:
+        lb = O.LocalBlend.__new__(O.LocalBlend)
+        lb.th, lb.latent_hw = (0.3, 0.3), (H, W)
+        mask = lb.mask_from_word_maps((acc / np.float32(40)).reshape(P, F, 16, 16), True)
+        ref = O.blend_latents(prev, mask)
+    else:
+        ref = prev
+    prev_t = t - 20
+    a_t = d.alphas_cumprod[t]
+    a_p = d.alphas_cumprod[prev_t] if prev_t >= 0 else d.final_alpha_cumprod
+    consts = (np.sqrt(np.float32(1) - a_t), np.sqrt(a_t), np.sqrt(np.float32(1) - a_p - np.float32(0)), np.sqrt(a_p))
+    out = ops.step_fused(torch.from_numpy(noise).to(DEV), torch.from_numpy(lat).to(DEV), consts, 7.5, True, fast,
+                         lb_acc=torch.from_numpy(acc).to(DEV) if blend else None, lb_count=40.0, lb_th=0.3)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def test_step_fused_inplace_and_nocfg():
+    from vp2p import ops
+    P, C, F, H, W = 1, 4, 2, 32, 32
+    g = np.random.default_rng(99)
+    noise = g.standard_normal((P, C, F, H, W)).astype(np.float32)
+    lat = g.standard_normal((P, C, F, H, W)).astype(np.float32)
+    d = O.DDIM()
+    d.set_timesteps(50)
+    ref = d.next_step(noise, 21, lat)
+    cur, nxt = 1, 21
+    consts = (np.sqrt(np.float32(1) - d.alphas_cumprod[cur]), np.sqrt(d.alphas_cumprod[cur]),
+              np.sqrt(np.float32(1) - d.alphas_cumprod[nxt]), np.sqrt(d.alphas_cumprod[nxt]))
+    x = torch.from_numpy(lat).to(DEV)
+    ops.step_fused(torch.from_numpy(noise).to(DEV), x, consts, cfg=False, out=x)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(x.cpu().numpy(), ref)

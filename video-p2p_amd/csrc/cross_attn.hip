@@ -1,0 +1,411 @@
+// K2 — hooked cross-attention over the <=128 text tokens with the P2P edit fused into the softmax
+// epilogue.
+//
+// Reference path (one call per attn2 layer, 16 per UNet forward):
+//   ptp_utils.py:206-220   q/k/v heads->batch, sim = q k^T * scale, softmax, controller, attn @ v
+//   run_videop2p.py:212-224  the controller edits only the conditional half attn[h//2:]
+//   run_videop2p.py:304-317  AttentionControlEdit.forward: per word w of each edited prompt
+//        new[w] = alpha_t[w] * R[w] + (1 - alpha_t[w]) * P_edit[w]
+//        R      = Replace: sum_j P_src[j] * M[j, w]                           (:333-334)
+//                 Refine : P_src[mapper[w]] * a[w] + P_edit[w] * (1 - a[w])   (:344-347)
+//                 Reweight wraps either: R * eq[w]                            (:359-363)
+//   run_videop2p.py:255-268  AttentionStore keeps the post-edit conditional maps (N <= 32^2),
+//        summed over steps; LocalBlend only ever reads sum_w alpha_lb[p][w] * maps of the res-16
+//        layers (:131-146), so this kernel accumulates exactly that reduction (lb_acc) instead.
+//
+// The reference materialises probs (B*f*h, N, 77) and makes ~6-8 elementwise passes over them.
+// Here one workgroup owns 32 query tokens of one CFG half for all heads and prompts: the source
+// prompt's probabilities are parked in LDS (fp32) while the edited prompts are computed, so the
+// edit is a handful of LDS reads per word and nothing but Q in / O out touches HBM.
+// The 77-token K/V (identical for all frames: attention.py:95 repeats the context per frame) are
+// pre-laid-out once per layer by vp2p_cross_kv_prep into MFMA fragment order and read through L1/L2.
+#include "common.hpp"
+#include "vp2p.h"
+
+namespace vp2p {
+
+template <typename T, int D>
+struct CrossCfg {
+  static constexpr bool BF = sizeof(T) == 2;
+  static constexpr int KD = Mfma<T>::KD;
+  static constexpr int DP = round_up(D, KD);
+  static constexpr int KS = DP / KD;
+  static constexpr int DV = round_up(D, 32);
+  static constexpr int NT = DV / 32;
+};
+
+// Workspace layout for KB key blocks (KP = 32*KB padded keys), per (b, head):
+//   K  : [KP][DP]  zero padded                                  (row = key)
+//   V  : bf16 -> [DV][KP] with keys permuted inside each 16-key group so that one lane's PV
+//                 A fragment (keys 8(j>>2) + 4h + (j&3), j = 0..7) is 16 contiguous bytes
+//        f32  -> [KP][DV] row-major
+template <typename T>
+__host__ __device__ inline int64_t cross_ws_elems(int batch, int heads, int kp, int dp, int dv) {
+  return (int64_t)batch * heads * kp * (dp + dv);
+}
+
+template <typename T, int D>
+__global__ void cross_kv_prep_kernel(const T* __restrict__ k, const T* __restrict__ v, int64_t k_sb,
+                                     int64_t k_sn, int64_t v_sb, int64_t v_sn, int batch, int nkv,
+                                     int heads, int kp, T* __restrict__ ws) {
+  using C = CrossCfg<T, D>;
+  const int64_t kelems = (int64_t)batch * heads * kp * C::DP;
+  const int64_t total = kelems + (int64_t)batch * heads * kp * C::DV;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    T val = (T)0.f;
+    if (i < kelems) {
+      const int c = (int)(i % C::DP);
+      const int64_t rowi = i / C::DP;
+      const int key = (int)(rowi % kp);
+      const int bh = (int)(rowi / kp);
+      const int b = bh / heads, head = bh % heads;
+      if (key < nkv && c < D) val = k[b * k_sb + key * k_sn + head * D + c];
+    } else {
+      const int64_t j = i - kelems;
+      int key, c, bh;
+      if constexpr (C::BF) {
+        const int slot = (int)(j % kp);
+        const int64_t rowi = j / kp;
+        c = (int)(rowi % C::DV);
+        bh = (int)(rowi / C::DV);
+        const int grp = slot >> 4, pos = slot & 15, hh = pos >> 3, jj = pos & 7;
+        key = 16 * grp + 8 * (jj >> 2) + 4 * hh + (jj & 3);
+      } else {
+        c = (int)(j % C::DV);
+        const int64_t rowi = j / C::DV;
+        key = (int)(rowi % kp);
+        bh = (int)(rowi / kp);
+      }
+      const int b = bh / heads, head = bh % heads;
+      if (key < nkv && c < D) val = v[b * v_sb + key * v_sn + head * D + c];
+    }
+    ws[i] = val;
+  }
+}
+
+template <typename T, int D, int KB>
+__global__ __launch_bounds__(256) void cross_attn_kernel(const vp2p_cross_attn_args a) {
+  using M = Mfma<T>;
+  using C = CrossCfg<T, D>;
+  constexpr int KP = 32 * KB;
+  constexpr int PROW = KP + 1;                 // fp32 source-prob row in LDS (odd: conflict-free)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* psrc_all = reinterpret_cast<float*>(smem);                 // [4 waves][32][PROW]
+  float* lbred = psrc_all + 4 * 32 * PROW;                          // [4 waves][4 prompts][32]
+
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int FQ = a.frames * a.tokens_q;
+  const int qblocks = (FQ + 31) >> 5;
+  const bool p2p = a.prompts > 0 && a.batch == 2 * a.prompts;
+  const int RP = p2p ? a.prompts : 1;          // rows per group
+  const int g = blockIdx.x / qblocks;          // group: CFG half (p2p) or batch row
+  const int qb = blockIdx.x - g * qblocks;
+  const bool cond = p2p && g == 1;
+  const bool edit = cond && (a.edit_mode != VP2P_EDIT_NONE || a.reweight);
+  const bool lb = cond && a.lb_acc != nullptr;
+  const int NKV = a.tokens_kv;
+
+  const int qi = qb * 32 + r;
+  const bool qv = qi < FQ;
+  const int fr = qv ? qi / a.tokens_q : 0;
+  const int pos = qv ? qi - fr * a.tokens_q : 0;
+  float* psrc = psrc_all + w * 32 * PROW + r * PROW;
+  const float cs = a.scale * kLog2e;
+  const T* ws = static_cast<const T*>(a.kv_ws);
+  const int64_t kelems = (int64_t)a.batch * a.heads * KP * C::DP;
+
+  float lbsum[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int head = w; head < a.heads; head += 4) {
+    for (int p = 0; p < RP; ++p) {
+      const int b = g * RP + p;
+      const T* qrow = static_cast<const T*>(a.q) + b * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * D;
+      typename M::frag qf[C::KS];
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) qf[s] = qv ? M::row_frag(qrow, s, h, D) : M::zero();
+
+      const T* kb_base = ws + ((int64_t)(b * a.heads + head) * KP) * C::DP;
+      f32x16 sc[KB];
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        sc[kb] = zero16();
+        const T* krow = kb_base + (kb * 32 + r) * C::DP;
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) {
+          typename M::frag af;
+          if constexpr (C::BF) af = *reinterpret_cast<const bf16x8*>(krow + 16 * s + 8 * h);
+          else af = krow[2 * s + h];
+          sc[kb] = M::mma(af, qf[s], sc[kb]);
+        }
+      }
+      // row softmax over the valid keys (the reference's global max gives the same probabilities
+      // wherever it does not underflow: ptp_utils.py:217)
+      float mx = kNegInf;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float v = (kb * 32 + acc_row(i, h) < NKV) ? sc[kb][i] * cs : kNegInf;
+          sc[kb][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, xhalf(mx));
+      float sum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float e = fast_exp2(sc[kb][i] - mx);
+          sc[kb][i] = e;
+          sum += e;
+        }
+      sum += xhalf(sum);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[kb][i] *= inv;
+
+      if (edit) {
+        if (p == 0) {
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) psrc[kb * 32 + acc_row(i, h)] = sc[kb][i];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+#pragma clang fp contract(off)
+          const int pe = p - 1;
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int wd = kb * 32 + acc_row(i, h);
+              if (wd < NKV) {
+                const float pe_val = sc[kb][i];
+                float R;
+                if (a.edit_mode == VP2P_EDIT_REPLACE) {
+                  const int* ptr = a.map_ptr + pe * (NKV + 1);
+                  float gsum = 0.f;
+                  for (int n = ptr[wd]; n < ptr[wd + 1]; ++n) gsum += psrc[a.map_idx[n]] * a.map_val[n];
+                  R = gsum;
+                } else if (a.edit_mode == VP2P_EDIT_REFINE) {
+                  const float ra = a.refine_alpha[pe * NKV + wd];
+                  const float gth = psrc[a.map_idx[pe * NKV + wd]];
+                  R = gth * ra + pe_val * (1.f - ra);
+                } else {
+                  R = psrc[wd];
+                }
+                if (a.reweight) R = R * a.equalizer[wd];
+                const float aw = a.alpha_words[pe * NKV + wd];
+                sc[kb][i] = R * aw + (1.f - aw) * pe_val;
+              }
+            }
+        }
+      }
+      if (lb) {
+        float part = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) part += a.lb_word_alpha[p * NKV + wd] * sc[kb][i];
+          }
+        lbsum[p & 3] += part + xhalf(part);
+      }
+      if (a.probs_out && qv) {
+        float* prow = a.probs_out + ((((int64_t)b * a.frames + fr) * a.heads + head) * a.tokens_q + pos) * NKV;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) prow[wd] = sc[kb][i];
+          }
+      }
+
+      // O^T = V^T P^T over the padded keys (P is exactly 0 there)
+      const T* vb_base = ws + kelems + ((int64_t)(b * a.heads + head) * KP) * C::DV;
+      f32x16 o[C::NT];
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t) o[t] = zero16();
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int sp = 0; sp < M::PV_STEPS; ++sp) {
+          const typename M::frag pf = M::p_frag(sc[kb], sp);
+#pragma unroll
+          for (int t = 0; t < C::NT; ++t) {
+            typename M::frag vf;
+            if constexpr (C::BF)
+              vf = *reinterpret_cast<const bf16x8*>(vb_base + (int64_t)(32 * t + r) * KP + kb * 32 + 16 * sp + 8 * h);
+            else
+              vf = vb_base[(int64_t)(kb * 32 + f32_pv_key(sp, h)) * C::DV + 32 * t + r];
+            o[t] = M::mma(vf, pf, o[t]);
+          }
+        }
+      if (qv) {
+        T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const int dc = 32 * t + 8 * gq + 4 * h;
+            if (dc < D) {
+              if constexpr (C::BF) {
+                bf16x4 v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (bf16)o[t][4 * gq + j];
+                *reinterpret_cast<bf16x4*>(orow + dc) = v;
+              } else {
+                f32x4 v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = o[t][4 * gq + j];
+                *reinterpret_cast<f32x4*>(orow + dc) = v;
+              }
+            }
+          }
+      }
+    }
+  }
+
+  if (lb) {  // deterministic head reduction across the 4 waves; one read-modify-write per token
+    if (h == 0)
+      for (int p = 0; p < RP && p < 4; ++p) lbred[(w * 4 + p) * 32 + r] = lbsum[p];
+    __syncthreads();
+    if (w == 0 && h == 0 && qv) {
+      for (int p = 0; p < RP && p < 4; ++p) {
+        const float tot = lbred[(0 * 4 + p) * 32 + r] + lbred[(1 * 4 + p) * 32 + r] +
+                          lbred[(2 * 4 + p) * 32 + r] + lbred[(3 * 4 + p) * 32 + r];
+        a.lb_acc[((int64_t)p * a.frames + fr) * a.tokens_q + pos] += tot;
+      }
+    }
+  }
+}
+
+template <typename T, int D>
+static int cross_dims(int& dp, int& dv) {
+  dp = CrossCfg<T, D>::DP;
+  dv = CrossCfg<T, D>::DV;
+  return 0;
+}
+
+static int cross_pad_dims(int head_dim, int dtype, int& dp, int& dv) {
+#define VP2P_DIMS(DIM) \
+  case DIM: return dtype == VP2P_BF16 ? cross_dims<bf16, DIM>(dp, dv) : cross_dims<float, DIM>(dp, dv);
+  switch (head_dim) {
+    VP2P_DIMS(32) VP2P_DIMS(40) VP2P_DIMS(64) VP2P_DIMS(80) VP2P_DIMS(128) VP2P_DIMS(160)
+    default: return VP2P_E_HEAD_DIM;
+  }
+#undef VP2P_DIMS
+}
+
+template <typename T, int D, int KB>
+static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
+  constexpr int KP = 32 * KB;
+  const int FQ = a->frames * a->tokens_q;
+  const bool p2p = a->prompts > 0 && a->batch == 2 * a->prompts;
+  const int groups = p2p ? 2 : a->batch;
+  const int64_t nwg = (int64_t)groups * ((FQ + 31) / 32);
+  if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+  const size_t lds = (4 * 32 * (KP + 1) + 4 * 4 * 32) * sizeof(float);
+  hipLaunchKernelGGL((cross_attn_kernel<T, D, KB>), dim3((unsigned)nwg), dim3(256), lds, s, *a);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+template <typename T, int D>
+static int launch_cross_kb(const vp2p_cross_attn_args* a, hipStream_t s) {
+  switch ((a->tokens_kv + 31) / 32) {
+    case 1: return launch_cross<T, D, 1>(a, s);
+    case 2: return launch_cross<T, D, 2>(a, s);
+    case 3: return launch_cross<T, D, 3>(a, s);
+    case 4: return launch_cross<T, D, 4>(a, s);
+    default: return VP2P_E_SHAPE;
+  }
+}
+
+template <typename T, int D>
+static int launch_prep(const void* k, const void* v, int64_t k_sb, int64_t k_sn, int64_t v_sb,
+                       int64_t v_sn, int batch, int nkv, int heads, void* ws, hipStream_t s) {
+  using C = CrossCfg<T, D>;
+  const int kp = 32 * ((nkv + 31) / 32);
+  const int64_t total = cross_ws_elems<T>(batch, heads, kp, C::DP, C::DV);
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL((cross_kv_prep_kernel<T, D>), dim3((unsigned)blocks), dim3(256), 0, s,
+                     static_cast<const T*>(k), static_cast<const T*>(v), k_sb, k_sn, v_sb, v_sn,
+                     batch, nkv, heads, kp, static_cast<T*>(ws));
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+}  // namespace vp2p
+
+using namespace vp2p;
+
+extern "C" int64_t vp2p_cross_kv_workspace_bytes(int32_t batch, int32_t tokens_kv, int32_t heads,
+                                                 int32_t head_dim, int32_t dtype) {
+  if (batch <= 0 || tokens_kv <= 0 || heads <= 0) return VP2P_E_ARG;
+  if (tokens_kv > 128) return VP2P_E_SHAPE;
+  if (dtype != VP2P_BF16 && dtype != VP2P_F32) return VP2P_E_DTYPE;
+  int dp = 0, dv = 0;
+  const int rc = cross_pad_dims(head_dim, dtype, dp, dv);
+  if (rc) return rc;
+  const int kp = 32 * ((tokens_kv + 31) / 32);
+  return (int64_t)batch * heads * kp * (dp + dv) * (dtype == VP2P_BF16 ? 2 : 4);
+}
+
+extern "C" int vp2p_cross_kv_prep(const void* k, const void* v, int64_t k_sb, int64_t k_sn,
+                                  int64_t v_sb, int64_t v_sn, int32_t batch, int32_t tokens_kv,
+                                  int32_t heads, int32_t head_dim, int32_t dtype, void* kv_ws,
+                                  void* stream) {
+  if (!k || !v || !kv_ws || batch <= 0 || tokens_kv <= 0 || heads <= 0) return VP2P_E_ARG;
+  if (tokens_kv > 128) return VP2P_E_SHAPE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define VP2P_PREP(DIM)                                                                          \
+  case DIM:                                                                                      \
+    return dtype == VP2P_BF16                                                                    \
+               ? launch_prep<bf16, DIM>(k, v, k_sb, k_sn, v_sb, v_sn, batch, tokens_kv, heads, kv_ws, s) \
+               : launch_prep<float, DIM>(k, v, k_sb, k_sn, v_sb, v_sn, batch, tokens_kv, heads, kv_ws, s);
+  if (dtype != VP2P_BF16 && dtype != VP2P_F32) return VP2P_E_DTYPE;
+  switch (head_dim) {
+    VP2P_PREP(32) VP2P_PREP(40) VP2P_PREP(64) VP2P_PREP(80) VP2P_PREP(128) VP2P_PREP(160)
+    default: return VP2P_E_HEAD_DIM;
+  }
+#undef VP2P_PREP
+}
+
+extern "C" int vp2p_cross_attn_p2p_fwd(const vp2p_cross_attn_args* a, void* stream) {
+  if (!a || !a->q || !a->kv_ws || !a->o) return VP2P_E_ARG;
+  if (a->batch <= 0 || a->frames <= 0 || a->tokens_q <= 0 || a->tokens_kv <= 0 || a->heads <= 0)
+    return VP2P_E_ARG;
+  if (a->tokens_kv > 128) return VP2P_E_SHAPE;
+  const int esz = a->dtype == VP2P_BF16 ? 2 : (a->dtype == VP2P_F32 ? 4 : 0);
+  if (!esz) return VP2P_E_DTYPE;
+  const int epc = 16 / esz;
+  const int64_t strides[] = {a->q_sb, a->q_sf, a->q_sn, a->o_sb, a->o_sf, a->o_sn};
+  for (int64_t st : strides)
+    if (st % epc) return VP2P_E_ARG;
+  if (a->head_dim % epc || (reinterpret_cast<uintptr_t>(a->q) & 15) || (reinterpret_cast<uintptr_t>(a->o) & 15))
+    return VP2P_E_ARG;
+  const bool p2p = a->prompts > 0 && a->batch == 2 * a->prompts;
+  if (p2p && a->prompts > 4) return VP2P_E_SHAPE;
+  const bool edit = p2p && (a->edit_mode != VP2P_EDIT_NONE || a->reweight);
+  if (edit) {
+    if (!a->alpha_words) return VP2P_E_ARG;
+    if (a->edit_mode == VP2P_EDIT_REPLACE && (!a->map_ptr || !a->map_idx || !a->map_val)) return VP2P_E_ARG;
+    if (a->edit_mode == VP2P_EDIT_REFINE && (!a->map_idx || !a->refine_alpha)) return VP2P_E_ARG;
+    if (a->reweight && !a->equalizer) return VP2P_E_ARG;
+  }
+  if (a->lb_acc && (!p2p || !a->lb_word_alpha)) return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define VP2P_CROSS(DIM) \
+  case DIM: return a->dtype == VP2P_BF16 ? launch_cross_kb<bf16, DIM>(a, s) : launch_cross_kb<float, DIM>(a, s);
+  switch (a->head_dim) {
+    VP2P_CROSS(32) VP2P_CROSS(40) VP2P_CROSS(64) VP2P_CROSS(80) VP2P_CROSS(128) VP2P_CROSS(160)
+    default: return VP2P_E_HEAD_DIM;
+  }
+#undef VP2P_CROSS
+}

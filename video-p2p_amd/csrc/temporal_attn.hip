@@ -1,0 +1,217 @@
+// K3 — hooked temporal attention (attn_temp) + replace_self_attention.
+//
+// Reference path: BasicTransformerBlock rearranges '(b f) d c -> (b d) f c' (attention.py:262-268),
+// the hooked forward (ptp_utils.py:196-221) computes an f x f softmax per (b, token, head) and the
+// controller, for steps in [0, int(50 * self_replace_steps)), overwrites the edited prompts'
+// conditional maps with the source prompt's (run_videop2p.py:293-298, 306, 315) before attn @ v.
+//
+// Here no rearrange is materialised: Q/K/V/O are addressed in place through (b, frame, token)
+// strides.  One 32-lane MFMA tile packs G = 32 / fpad tokens x fpad frames (fpad = next power of
+// two >= f); cross-token scores are masked to -inf, so one 32x32x16 product serves G tokens.
+// The source prompt's probability fragments stay in registers and are fed straight to the edited
+// prompts' P.V products: the self-replace is free.
+#include "common.hpp"
+#include "vp2p.h"
+
+namespace vp2p {
+
+template <typename T, int D>
+struct TempCfg {
+  static constexpr bool BF = sizeof(T) == 2;
+  static constexpr int KD = Mfma<T>::KD;
+  static constexpr int DP = round_up(D, KD);
+  static constexpr int KS = DP / KD;
+  static constexpr int DV = round_up(D, 32);
+  static constexpr int NT = DV / 32;
+  static constexpr int EPC = 16 / (int)sizeof(T);
+  static constexpr int CPR = D / EPC;
+  static constexpr int vrow_bf16() {
+    int v = DV;
+    while (!((v / 2) % 64 == 16 || (v / 2) % 64 == 48)) v += 8;
+    return v;
+  }
+  static constexpr int VROW = BF ? vrow_bf16() : DV;
+  static constexpr int WAVE_LDS = 32 * VROW * (int)sizeof(T);
+};
+
+template <typename T, int D>
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void temporal_attn_kernel(const vp2p_temporal_attn_args a, int lf) {
+  using M = Mfma<T>;
+  using C = TempCfg<T, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  T* Vs = reinterpret_cast<T*>(smem + w * C::WAVE_LDS);
+  for (int i = l; i < C::WAVE_LDS / 16; i += 64) reinterpret_cast<u32x4*>(Vs)[i] = u32x4{0, 0, 0, 0};
+
+  const int fpad = 1 << lf, G = 32 >> lf;
+  const int F = a.frames, N = a.tokens;
+  const int pblocks = (N + G - 1) / G;
+  const bool p2p = a.prompts > 0 && a.batch == 2 * a.prompts;
+  const int RP = p2p ? a.prompts : 1;
+  const int g = blockIdx.x / pblocks;
+  const int pb = blockIdx.x - g * pblocks;
+  const bool replace = p2p && g == 1 && a.self_replace;
+
+  // this lane's (token slot, frame) as a query row, and as the key row of the same index
+  const int slot = r >> lf, fr = r & (fpad - 1);
+  const int pos = pb * G + slot;
+  const bool rv = fr < F && pos < N;
+  const float cs = a.scale * kLog2e;
+
+  for (int head = w; head < a.heads; head += 4) {
+    typename M::frag psrc[M::PV_STEPS];
+    f32x16 prob_src;
+    for (int p = 0; p < RP; ++p) {
+      const int b = g * RP + p;
+      const int64_t qoff = rv ? b * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * D : 0;
+      const int64_t koff = rv ? b * a.k_sb + fr * a.k_sf + pos * a.k_sn + head * D : 0;
+      const int64_t voff = rv ? b * a.v_sb + fr * a.v_sf + pos * a.v_sn + head * D : 0;
+      f32x16 sc;
+      typename M::frag pf[M::PV_STEPS];
+      if (replace && p > 0) {
+#pragma unroll
+        for (int sp = 0; sp < M::PV_STEPS; ++sp) pf[sp] = psrc[sp];
+        sc = prob_src;
+      } else {
+        const T* qrow = static_cast<const T*>(a.q) + qoff;
+        const T* krow = static_cast<const T*>(a.k) + koff;
+        sc = zero16();
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) {
+          const typename M::frag qf = rv ? M::row_frag(qrow, s, h, D) : M::zero();
+          const typename M::frag kf = rv ? M::row_frag(krow, s, h, D) : M::zero();
+          sc = M::mma(kf, qf, sc);
+        }
+        float mx = kNegInf;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kk = acc_row(i, h);
+          const bool ok = (kk >> lf) == slot && (kk & (fpad - 1)) < F;
+          const float v = ok ? sc[i] * cs : kNegInf;
+          sc[i] = v;
+          mx = fmaxf(mx, v);
+        }
+        mx = fmaxf(mx, xhalf(mx));
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float e = fast_exp2(sc[i] - mx);
+          sc[i] = e;
+          sum += e;
+        }
+        sum += xhalf(sum);
+        const float inv = 1.f / sum;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[i] *= inv;
+#pragma unroll
+        for (int sp = 0; sp < M::PV_STEPS; ++sp) pf[sp] = M::p_frag(sc, sp);
+        if (replace) {
+#pragma unroll
+          for (int sp = 0; sp < M::PV_STEPS; ++sp) psrc[sp] = pf[sp];
+          prob_src = sc;
+        }
+      }
+      if (a.probs_out && rv) {
+        float* prow = a.probs_out + ((((int64_t)b * N + pos) * a.heads + head) * F + fr) * F;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kk = acc_row(i, h);
+          if ((kk >> lf) == slot && (kk & (fpad - 1)) < F) prow[kk & (fpad - 1)] = sc[i];
+        }
+      }
+
+      // stage this tile's 32 V rows (row index = lane row r) in the wave's LDS image
+      __builtin_amdgcn_wave_barrier();
+      {
+        const T* vrow = static_cast<const T*>(a.v) + voff;
+        for (int c = h; c < C::CPR; c += 2) {
+          const u32x4 val = rv ? *reinterpret_cast<const u32x4*>(vrow + c * C::EPC) : u32x4{0, 0, 0, 0};
+          *reinterpret_cast<u32x4*>(Vs + r * C::VROW + c * C::EPC) = val;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+      f32x16 o[C::NT];
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t) o[t] = zero16();
+#pragma unroll
+      for (int sp = 0; sp < M::PV_STEPS; ++sp)
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t) {
+          typename M::frag vf;
+          if constexpr (C::BF) vf = vt_frag_lds<C::VROW>(Vs, 0, sp, t);
+          else vf = Vs[f32_pv_key(sp, h) * C::VROW + 32 * t + r];
+          o[t] = M::mma(vf, pf[sp], o[t]);
+        }
+      if (rv) {
+        T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const int dc = 32 * t + 8 * gq + 4 * h;
+            if (dc < D) {
+              if constexpr (C::BF) {
+                bf16x4 v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (bf16)o[t][4 * gq + j];
+                *reinterpret_cast<bf16x4*>(orow + dc) = v;
+              } else {
+                f32x4 v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = o[t][4 * gq + j];
+                *reinterpret_cast<f32x4*>(orow + dc) = v;
+              }
+            }
+          }
+      }
+    }
+  }
+}
+
+template <typename T, int D>
+static int launch_temporal(const vp2p_temporal_attn_args* a, hipStream_t s) {
+  using C = TempCfg<T, D>;
+  int lf = 0;
+  while ((1 << lf) < a->frames) ++lf;
+  const int G = 32 >> lf;
+  const bool p2p = a->prompts > 0 && a->batch == 2 * a->prompts;
+  const int groups = p2p ? 2 : a->batch;
+  const int64_t nwg = (int64_t)groups * ((a->tokens + G - 1) / G);
+  if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+  hipLaunchKernelGGL((temporal_attn_kernel<T, D>), dim3((unsigned)nwg), dim3(256), 4 * C::WAVE_LDS, s, *a, lf);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+}  // namespace vp2p
+
+using namespace vp2p;
+
+extern "C" int vp2p_temporal_attn_p2p_fwd(const vp2p_temporal_attn_args* a, void* stream) {
+  if (!a || !a->q || !a->k || !a->v || !a->o) return VP2P_E_ARG;
+  if (a->batch <= 0 || a->frames <= 0 || a->tokens <= 0 || a->heads <= 0 || a->head_dim <= 0)
+    return VP2P_E_ARG;
+  if (a->frames > 32) return VP2P_E_SHAPE;
+  const int esz = a->dtype == VP2P_BF16 ? 2 : (a->dtype == VP2P_F32 ? 4 : 0);
+  if (!esz) return VP2P_E_DTYPE;
+  const int epc = 16 / esz;
+  const int64_t strides[] = {a->q_sb, a->q_sf, a->q_sn, a->k_sb, a->k_sf, a->k_sn,
+                             a->v_sb, a->v_sf, a->v_sn, a->o_sb, a->o_sf, a->o_sn};
+  for (int64_t st : strides)
+    if (st % epc) return VP2P_E_ARG;
+  const void* ptrs[] = {a->q, a->k, a->v, a->o};
+  for (const void* p : ptrs)
+    if (reinterpret_cast<uintptr_t>(p) & 15) return VP2P_E_ARG;
+  if (a->head_dim % epc) return VP2P_E_ARG;
+  if (a->self_replace && !(a->prompts > 0 && a->batch == 2 * a->prompts)) return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define VP2P_TEMP(DIM) \
+  case DIM: return a->dtype == VP2P_BF16 ? launch_temporal<bf16, DIM>(a, s) : launch_temporal<float, DIM>(a, s);
+  switch (a->head_dim) {
+    VP2P_TEMP(32) VP2P_TEMP(40) VP2P_TEMP(64) VP2P_TEMP(80) VP2P_TEMP(128) VP2P_TEMP(160)
+    default: return VP2P_E_HEAD_DIM;
+  }
+#undef VP2P_TEMP
+}

@@ -1,0 +1,241 @@
+"""Torch-facing wrappers over the C ABI (torch supplies device memory and the stream only).
+
+Every op here launches a HIP kernel from libvp2p_hip.so on ``torch.cuda.current_stream()``;
+there is no CPU path.  Shapes follow the reference's tensors:
+
+* ``(b f)`` activations: ``(B*f, N, C)`` rows ordered batch-major, frame-minor (attention.py:94)
+* ``(b d)`` activations: ``(B*N, f, C)`` (the temporal rearrange, attention.py:263)
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import check
+
+_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
+
+
+def _dtype(*ts):
+    d = ts[0].dtype
+    for t in ts:
+        if t.dtype != d:
+            raise TypeError(f"dtype mismatch: {[x.dtype for x in ts]}")
+        if not t.is_cuda:
+            raise RuntimeError("vp2p ops run on the GPU only (tensor on %s)" % t.device)
+        if t.stride(-1) != 1:
+            raise ValueError("channel dimension must be contiguous")
+    if d not in _DT:
+        raise TypeError(f"unsupported dtype {d}")
+    return _DT[d]
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _bf_strides(t: torch.Tensor, frames: int):
+    """(b, f, n) element strides of a '(b f) n c' tensor."""
+    s0, s1 = t.stride(0), t.stride(1)
+    return frames * s0, s0, s1
+
+
+def _bd_strides(t: torch.Tensor, tokens: int):
+    """(b, f, n) element strides of a '(b d) f c' tensor."""
+    s0, s1 = t.stride(0), t.stride(1)
+    return tokens * s0, s1, s0
+
+
+# ----------------------------------------------------------------------------------------------
+def frame_attention(q: torch.Tensor, k0: torch.Tensor, v0: torch.Tensor, frames: int, heads: int,
+                    scale: Optional[float] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """FrameAttention core (attention.py:282-322).  q: (B*f, N, C); k0, v0: frame-0 keys/values
+    (B, Nk, C) -- or full (B*f, Nk, C) tensors, of which only frame 0 is read."""
+    dt = _dtype(q, k0, v0)
+    Bf, N, C = q.shape
+    B = Bf // frames
+    if B * frames != Bf or C % heads:
+        raise ValueError("bad shapes")
+    if out is None:
+        out = torch.empty_like(q, memory_format=torch.contiguous_format)
+    d = C // heads
+    k_sb = k0.stride(0) * (frames if k0.shape[0] == Bf else 1)
+    v_sb = v0.stride(0) * (frames if v0.shape[0] == Bf else 1)
+    if k0.shape[0] not in (B, Bf) or v0.shape[0] != k0.shape[0]:
+        raise ValueError("k0/v0 must be (B, Nk, C) or (B*f, Nk, C)")
+    q_sb, q_sf, q_sn = _bf_strides(q, frames)
+    o_sb, o_sf, o_sn = _bf_strides(out, frames)
+    a = _lib.FrameAttnArgs(_ptr(q), _ptr(k0), _ptr(v0), _ptr(out), q_sb, q_sf, q_sn,
+                           k_sb, k0.stride(1), v_sb, v0.stride(1), o_sb, o_sf, o_sn,
+                           B, frames, N, k0.shape[1], heads, d,
+                           float(d ** -0.5 if scale is None else scale), dt)
+    check(_lib.load().vp2p_frame_attn_fwd(ctypes.byref(a), _stream()), "vp2p_frame_attn_fwd")
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+class CrossEditPlan:
+    """Device-resident descriptor of an AttentionControlEdit for the fused cross kernel.
+
+    Built once per controller (host work happens here, not per call): the per-step word alphas
+    (cross_replace_alpha, run_videop2p.py:325), the mapper as CSC (Replace) or a gather index
+    (Refine), the equalizer (Reweight) and LocalBlend's word weights."""
+
+    def __init__(self, prompts: int, edit_mode: int, reweight: bool, alpha_steps: torch.Tensor,
+                 mapper=None, refine_alpha=None, equalizer=None, lb_word_alpha=None,
+                 device="cuda", tokens_kv: int = 77):
+        self.prompts = prompts
+        self.edit_mode = edit_mode
+        self.reweight = bool(reweight)
+        self.tokens_kv = tokens_kv
+        dev = torch.device(device)
+        # (steps+1, P-1, 77) float32
+        self.alpha_steps = alpha_steps.reshape(alpha_steps.shape[0], prompts - 1, -1).float().contiguous().to(dev)
+        self.map_ptr = self.map_idx = self.map_val = self.refine_alpha = None
+        if edit_mode == _lib.EDIT_REPLACE:
+            m = torch.as_tensor(mapper, dtype=torch.float32).reshape(prompts - 1, tokens_kv, tokens_kv)
+            ptr, idx, val = [], [], []
+            for pe in range(prompts - 1):
+                base = len(idx)
+                ptr.append(base)
+                col_ptr = [base]
+                for w in range(tokens_kv):
+                    nz = torch.nonzero(m[pe, :, w]).flatten().tolist()
+                    idx.extend(nz)
+                    val.extend(m[pe, nz, w].tolist())
+                    col_ptr.append(len(idx))
+                ptr[-1:] = col_ptr
+            self.map_ptr = torch.tensor(ptr, dtype=torch.int32, device=dev)
+            self.map_idx = torch.tensor(idx or [0], dtype=torch.int32, device=dev)
+            self.map_val = torch.tensor(val or [0.0], dtype=torch.float32, device=dev)
+        elif edit_mode == _lib.EDIT_REFINE:
+            mp = torch.as_tensor(mapper, dtype=torch.int64).reshape(prompts - 1, tokens_kv)
+            self.map_idx = (mp % tokens_kv).to(torch.int32).contiguous().to(dev)  # -1 -> last word
+            self.refine_alpha = torch.as_tensor(refine_alpha, dtype=torch.float32).reshape(
+                prompts - 1, tokens_kv).contiguous().to(dev)
+        self.equalizer = (None if equalizer is None else
+                          torch.as_tensor(equalizer, dtype=torch.float32).reshape(-1)[:tokens_kv].contiguous().to(dev))
+        self.lb_word_alpha = (None if lb_word_alpha is None else
+                              torch.as_tensor(lb_word_alpha, dtype=torch.float32).reshape(prompts, tokens_kv).contiguous().to(dev))
+
+    def alpha_ptr(self, step: int):
+        return ctypes.c_void_p(self.alpha_steps[step].data_ptr())
+
+
+def cross_kv_prep(k: torch.Tensor, v: torch.Tensor, heads: int) -> torch.Tensor:
+    dt = _dtype(k, v)
+    B, nkv, C = k.shape
+    lib = _lib.load()
+    nbytes = lib.vp2p_cross_kv_workspace_bytes(B, nkv, heads, C // heads, dt)
+    if nbytes < 0:
+        check(int(nbytes), "vp2p_cross_kv_workspace_bytes")
+    ws = torch.empty(int(nbytes), dtype=torch.uint8, device=k.device)
+    check(lib.vp2p_cross_kv_prep(_ptr(k), _ptr(v), k.stride(0), k.stride(1), v.stride(0), v.stride(1),
+                                 B, nkv, heads, C // heads, dt, _ptr(ws), _stream()), "vp2p_cross_kv_prep")
+    return ws
+
+
+def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frames: int, heads: int,
+                        plan: Optional[CrossEditPlan] = None, step: int = 0, edit: bool = True,
+                        lb_acc: Optional[torch.Tensor] = None, probs_out: Optional[torch.Tensor] = None,
+                        scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
+                        prompts: int = 0) -> torch.Tensor:
+    """Hooked attn2 (ptp_utils.py:196-221) with the controller edit fused.  q: (B*f, N, C);
+    k, v: the projected context (B, Nk, C) shared by all frames of a batch row."""
+    dt = _dtype(q, k, v)
+    Bf, N, C = q.shape
+    B = Bf // frames
+    if k.shape[0] != B:
+        raise ValueError("k/v must be (B, Nk, C)")
+    d = C // heads
+    nkv = k.shape[1]
+    ws = cross_kv_prep(k, v, heads)
+    if out is None:
+        out = torch.empty_like(q, memory_format=torch.contiguous_format)
+    q_sb, q_sf, q_sn = _bf_strides(q, frames)
+    o_sb, o_sf, o_sn = _bf_strides(out, frames)
+    P = plan.prompts if plan is not None else prompts
+    mode = plan.edit_mode if (plan is not None and edit) else _lib.EDIT_NONE
+    rew = int(plan.reweight) if (plan is not None and edit) else 0
+    a = _lib.CrossAttnArgs(_ptr(q), _ptr(ws), _ptr(out), q_sb, q_sf, q_sn, o_sb, o_sf, o_sn,
+                           B, frames, N, nkv, heads, d, float(d ** -0.5 if scale is None else scale), dt,
+                           P, mode, rew,
+                           plan.alpha_ptr(step) if plan is not None else None,
+                           _ptr(plan.map_ptr) if plan is not None else None,
+                           _ptr(plan.map_idx) if plan is not None else None,
+                           _ptr(plan.map_val) if plan is not None else None,
+                           _ptr(plan.refine_alpha) if plan is not None else None,
+                           _ptr(plan.equalizer) if plan is not None else None,
+                           _ptr(lb_acc), _ptr(plan.lb_word_alpha) if (plan is not None and lb_acc is not None) else None,
+                           _ptr(probs_out))
+    check(_lib.load().vp2p_cross_attn_p2p_fwd(ctypes.byref(a), _stream()), "vp2p_cross_attn_p2p_fwd")
+    return out
+
+
+def temporal_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frames: int, heads: int,
+                           prompts: int = 0, self_replace: bool = False,
+                           probs_out: Optional[torch.Tensor] = None, scale: Optional[float] = None,
+                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Hooked attn_temp with replace_self_attention on '(b f) n c' tensors (B*f, N, C): the
+    temporal rearrange of attention.py:263 is expressed through strides, never materialised."""
+    dt = _dtype(q, k, v)
+    Bf, N, C = q.shape
+    B = Bf // frames
+    st = lambda t: _bf_strides(t, frames)  # noqa: E731
+    if out is None:
+        out = torch.empty_like(q, memory_format=torch.contiguous_format)
+    d = C // heads
+    a = _lib.TemporalAttnArgs(_ptr(q), _ptr(k), _ptr(v), _ptr(out), *st(q), *st(k), *st(v), *st(out),
+                              B, frames, N, heads, d, float(d ** -0.5 if scale is None else scale), dt,
+                              prompts, int(self_replace), _ptr(probs_out))
+    check(_lib.load().vp2p_temporal_attn_p2p_fwd(ctypes.byref(a), _stream()), "vp2p_temporal_attn_p2p_fwd")
+    return out
+
+
+def temporal_attention_p2p_bd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, heads: int,
+                              prompts: int = 0, self_replace: bool = False,
+                              probs_out: Optional[torch.Tensor] = None, scale: Optional[float] = None,
+                              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Same op on the reference's '(b d) f c' tensors (B*N, f, C)."""
+    dt = _dtype(q, k, v)
+    BN, F, C = q.shape
+    N = BN // batch
+    if out is None:
+        out = torch.empty_like(q, memory_format=torch.contiguous_format)
+    st = lambda t: _bd_strides(t, N)  # noqa: E731
+    d = C // heads
+    a = _lib.TemporalAttnArgs(_ptr(q), _ptr(k), _ptr(v), _ptr(out), *st(q), *st(k), *st(v), *st(out),
+                              batch, F, N, heads, d, float(d ** -0.5 if scale is None else scale), dt,
+                              prompts, int(self_replace), _ptr(probs_out))
+    check(_lib.load().vp2p_temporal_attn_p2p_fwd(ctypes.byref(a), _stream()), "vp2p_temporal_attn_p2p_fwd")
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+def step_fused(noise: torch.Tensor, latents: torch.Tensor, consts, guidance: float = 7.5, cfg: bool = True,
+               fast: bool = False, lb_acc: Optional[torch.Tensor] = None, lb_hw=(16, 16),
+               lb_count: float = 40.0, lb_th: float = 0.3, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """CFG + DDIM update + LocalBlend in one launch.  noise: (2P or P, C, f, H, W) bf16/f32,
+    latents: (P, C, f, H, W) fp32, consts = (c1, c2, c3, c4) float32 scalars."""
+    if not (noise.is_cuda and latents.is_cuda):
+        raise RuntimeError("step_fused runs on the GPU only")
+    if latents.dtype != torch.float32 or not latents.is_contiguous() or not noise.is_contiguous():
+        raise ValueError("latents must be contiguous fp32, noise contiguous")
+    P, C, F, H, W = latents.shape
+    if noise.shape[0] != (2 * P if cfg else P) or tuple(noise.shape[1:]) != (C, F, H, W):
+        raise ValueError(f"noise shape {tuple(noise.shape)} vs latents {tuple(latents.shape)}")
+    if out is None:
+        out = torch.empty_like(latents)
+    c1, c2, c3, c4 = (float(c) for c in consts)
+    a = _lib.StepArgs(_ptr(noise), _DT[noise.dtype], _ptr(latents), _ptr(out), P, C, F, H, W,
+                      int(cfg), int(fast), float(guidance), c1, c2, c3, c4,
+                      _ptr(lb_acc), int(lb_hw[0]), int(lb_hw[1]), float(lb_count), float(lb_th))
+    check(_lib.load().vp2p_step_fused(ctypes.byref(a), _stream()), "vp2p_step_fused")
+    return out
