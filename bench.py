@@ -1,0 +1,241 @@
+#!/usr/bin/env python
+"""Benchmark: edited frames/s of a 50-step DDIM Video-P2P edit at 512^2 (BASELINE.json metric).
+
+One "step" = one complete edit of one clip: 50 denoising steps of the UNet3D at batch 4
+(2 prompts x CFG) with the P2P controller (AttentionRefine + LocalBlend + AttentionReweight of
+configs/rabbit-jump-p2p.yaml), fast mode, DDIM eta = 0 -- configs[1] of BASELINE.json
+("rabbit-jump-p2p 8f 512^2 on 1xMI355X bf16").  Synthetic data: random-init SD-1.5-geometry
+UNet3D (seed 0, N(0, 0.02), attn_temp.to_out non-zero), random text embeddings standing in for
+CLIP (seed 1; CLIP and VAE are excluded from the metric), x_T ~ N(0, 1) (seed 2 + rank).
+
+Multi-GPU (torchrun): every rank edits its own clip, no data-path collective (scaling "weak");
+value = clips * frames / max-over-ranks wall time.
+
+The JSON line also carries the live roofline of K1 (frame attention, the dominant, MFMA-bound
+kernel: its res-64 launch timed with HIP events on the launch stream during the timed region) and
+a CPU baseline (rank 0, N = 1): the oracle's fp32 CPU path on a bounded per-block sample,
+extrapolated to the same edit.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "video-p2p_amd"))
+
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+RABBIT = (["a rabbit is jumping on the grass", "a origami rabbit is jumping on the grass"],
+          False, (("rabbit",), ("rabbit",)), {"words": ["origami"], "values": [2]}, 0.2, 0.5)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2, help="timed edits (each = 50 DDIM steps)")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--ddim-steps", type=int, default=50)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-k1-events", action="store_true")
+    return ap.parse_args()
+
+
+class K1Timer:
+    """Brackets every res-64 FrameAttention launch with HIP events on the launch stream."""
+
+    def __init__(self, ops, tokens=4096):
+        self.ops, self.tokens, self.orig = ops, tokens, ops.frame_attention
+        self.events, self.active = [], False
+
+    def __enter__(self):
+        orig = self.orig
+
+        def wrapped(q, *a, **k):
+            if not self.active or q.shape[1] != self.tokens:
+                return orig(q, *a, **k)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = orig(q, *a, **k)
+            e.record()
+            self.events.append((s, e, tuple(q.shape)))
+            return out
+
+        self.ops.frame_attention = wrapped
+        import vp2p.attention as att
+        att.ops.frame_attention = wrapped
+        return self
+
+    def __exit__(self, *exc):
+        self.ops.frame_attention = self.orig
+
+    def summary(self, frames, peak):
+        if not self.events:
+            return None
+        ms = [s.elapsed_time(e) for s, e, _ in self.events]
+        Bf, N, C = self.events[0][2]
+        flops = 4.0 * Bf * N * N * C           # QK^T + PV, frame-0 K/V: 4 * B*f * HW^2 * C
+        avg_s = sum(ms) / len(ms) / 1e3
+        achieved = flops / avg_s / 1e12
+        return {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel": "vp2p::frame_attn_kernel<bf16,40> (res-64 FrameAttention)",
+                "launches": len(ms), "avg_ms": round(sum(ms) / len(ms), 4),
+                "flops_per_launch": flops}
+
+
+def cpu_baseline(frames, ddim_steps, threads):
+    """Oracle fp32 CPU path on a bounded sample: one transformer block and one resnet block per
+    resolution level of the B=4 edit UNet, extrapolated by the block counts of one forward and x50."""
+    import numpy as np
+    from oracle import p2p_oracle as O
+    from oracle import unet_ref
+    from vp2p.tokenizer import SyntheticCLIPTokenizer
+    from vp2p.unet3d import UNet3DConditionModel, init_random_
+    torch.set_num_threads(threads)
+    prompts, swap, blend, eq, cross, self_ = RABBIT
+    tok = SyntheticCLIPTokenizer()
+    ctrl = O.EditController(prompts, swap, {"default_": cross}, self_, tok, blend_words=blend, eq_params=eq)
+    sd = {k: v for k, v in init_random_(UNet3DConditionModel(), seed=0).state_dict().items()}
+    g = torch.Generator().manual_seed(3)
+    B = 4
+    ctx = torch.randn(B, 77, 768, generator=g)
+    emb = torch.randn(B, 1280, generator=g)
+    # (prefix of a transformer, prefix of a resnet, channels, latent size, transformers, resnets per forward)
+    levels = [("down_blocks.0.attentions.0.", "down_blocks.0.resnets.1.", 320, 64, 5, 5),
+              ("down_blocks.1.attentions.0.", "down_blocks.1.resnets.1.", 640, 32, 5, 5),
+              ("down_blocks.2.attentions.0.", "down_blocks.2.resnets.1.", 1280, 16, 5, 5),
+              ("mid_block.attentions.0.", "mid_block.resnets.0.", 1280, 8, 1, 7)]
+    t_fwd, t_sample = 0.0, 0.0
+    for tp, rp, C, hw, n_t, n_r in levels:
+        x = torch.randn(B, C, frames, hw, hw, generator=g) * 0.5
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            unet_ref.transformer(sd, tp, x, ctx, ctrl, "down")
+        t1 = time.perf_counter()
+        with torch.no_grad():
+            unet_ref.resnet(sd, rp, x, emb)
+        t2 = time.perf_counter()
+        t_fwd += n_t * (t1 - t0) + n_r * (t2 - t1)
+        t_sample += t2 - t0
+    t_edit = t_fwd * ddim_steps
+    return {"value": round(frames / t_edit, 6), "unit": "edited frames/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle/unet_ref.py fp32 on host CPU: 1 transformer block + 1 resnet block per level "
+                       f"(B=4, f={frames}, 512^2) timed once ({t_sample:.1f} s), extrapolated by block counts to "
+                       f"one UNet forward ({t_fwd:.1f} s) x {ddim_steps} steps; excludes up/downsample convs"),
+            "cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import vp2p
+    from vp2p import ops
+    from vp2p.pipeline import VideoP2PPipeline
+    from vp2p.tokenizer import SyntheticCLIPTokenizer
+    from vp2p.unet3d import UNet3DConditionModel, init_random_
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    f = args.frames
+    prompts, swap, blend, eq, cross, self_ = RABBIT
+    tok = SyntheticCLIPTokenizer()
+    unet = init_random_(UNet3DConditionModel(), seed=0).to(dev, dtype).to(memory_format=torch.channels_last)
+    unet.eval()
+    ctrl = vp2p.make_controller(prompts, swap, {"default_": cross}, self_, blend, eq, tokenizer=tok,
+                                num_steps=args.ddim_steps)
+    vp2p.register_attention_control(type("Pipe", (), {"unet": unet})(), ctrl)
+    g = torch.Generator().manual_seed(1)
+    unc = torch.randn(1, 77, 768, generator=g)
+    emb = torch.cat([unc, unc, torch.randn(2, 77, 768, generator=g)]).to(dev)
+    x_T = torch.randn(1, 4, f, 64, 64, generator=torch.Generator().manual_seed(2 + rank)).to(dev)
+    pipe = VideoP2PPipeline(unet)
+
+    def edit():
+        ctrl.reset()
+        return pipe(prompts, f, latents=x_T, controller=ctrl, fast=True, text_embeddings=emb,
+                    num_inference_steps=args.ddim_steps)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = edit()
+        torch.cuda.synchronize()
+        timer = K1Timer(ops)
+        with timer:
+            timer.active = not args.no_k1_events
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                out = edit()
+            torch.cuda.synchronize()
+            barrier()
+            t1 = time.perf_counter()
+            timer.active = False
+    elapsed = t1 - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    finite = bool(torch.isfinite(out).all().item())
+    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
+    roof = timer.summary(f, peak)
+    result = {
+        "metric": "edited frames/sec, 50-step DDIM P2P 512^2; attn MFMA util % of gfx950 peak",
+        "value": round(f * args.steps * world / elapsed, 4),
+        "unit": "edited frames/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.dtype, "data": "synthetic (random-init SD-1.5-geometry UNet3D, random text embeddings, x_T~N(0,1))",
+        "config": {"workload": "rabbit-jump-p2p --fast: AttentionRefine+LocalBlend+Reweight, 8 frames 512^2, "
+                               f"{args.ddim_steps}-step DDIM, UNet batch 4", "frames": f, "resolution": 512,
+                   "ddim_steps": args.ddim_steps, "unet_batch": 4, "parallelism": f"clip-parallel x{world}"},
+        "roofline": roof,
+        "output_finite": finite,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(f, args.ddim_steps, min(16, os.cpu_count() or 1))
+        except Exception as e:  # keep the GPU line even if the host leg fails
+            result["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

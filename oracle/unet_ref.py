@@ -1,0 +1,157 @@
+"""CPU fp32 restatement of the tuneavideo UNet3D forward with the P2P hook.  TEST INFRASTRUCTURE
+ONLY (importable by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg).
+
+Functional form over a state dict (keys as tuneavideo checkpoints), written against the
+reference's semantics:
+  unet.py:279-414            time embedding, conv_in, down / mid / up wiring, conv_norm_out
+  unet_blocks.py:125-589     block wiring, skip order, up-block concatenation
+  resnet.py:11-205           inflated convs, 5-D GroupNorm (statistics over c/G x f x h x w)
+  attention.py:90-329        Transformer3DModel / BasicTransformerBlock / FrameAttention
+                             (first-frame K/V), the '(b f) d c -> (b d) f c' temporal rearrange
+  ptp_utils.py:196-221       hooked attn2 / attn_temp with the numpy oracle controller
+Dense layers use torch CPU fp32 (the reference's own ops); frame attention is chunked per
+(batch*frame) slab instead of materialising the (B*f*h, HW, HW) score tensor.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import p2p_oracle as O
+
+HEADS = 8
+
+
+def _conv_frames(x5: torch.Tensor, sd, p: str, stride: int = 1) -> torch.Tensor:
+    """InflatedConv3d: Conv2d over '(b f)' (resnet.py:11-19)."""
+    B, C, f, H, W = x5.shape
+    w = sd[p + "weight"]
+    y = F.conv2d(x5.permute(0, 2, 1, 3, 4).reshape(B * f, C, H, W), w, sd.get(p + "bias"),
+                 stride=stride, padding=w.shape[-1] // 2)
+    return y.reshape(B, f, *y.shape[1:]).permute(0, 2, 1, 3, 4)
+
+
+def _gn(x, sd, p, eps):
+    return F.group_norm(x, 32, sd[p + "weight"], sd[p + "bias"], eps)
+
+
+def _lin(x, sd, p):
+    return F.linear(x, sd[p + "weight"], sd.get(p + "bias"))
+
+
+def _ln(x, sd, p):
+    return F.layer_norm(x, (x.shape[-1],), sd[p + "weight"], sd[p + "bias"], 1e-5)
+
+
+def resnet(sd, p, x5, temb, eps=1e-5):
+    h = _conv_frames(F.silu(_gn(x5, sd, p + "norm1.", eps)), sd, p + "conv1.")
+    h = h + _lin(F.silu(temb), sd, p + "time_emb_proj.")[:, :, None, None, None]
+    h = _conv_frames(F.silu(_gn(h, sd, p + "norm2.", eps)), sd, p + "conv2.")
+    sc = _conv_frames(x5, sd, p + "conv_shortcut.") if (p + "conv_shortcut.weight") in sd else x5
+    return sc + h
+
+
+def frame_attention(sd, p, x, f):
+    """attention.py:273-329 on (B*f, N, C)."""
+    Bf, N, C = x.shape
+    B = Bf // f
+    q = _lin(x, sd, p + "to_q.")
+    x0 = x.reshape(B, f, N, C)[:, 0]
+    k = _lin(x0, sd, p + "to_k.")
+    v = _lin(x0, sd, p + "to_v.")
+    d = C // HEADS
+    out = torch.empty_like(q)
+    for b in range(B):
+        kb = k[b].reshape(N, HEADS, d).permute(1, 0, 2)
+        vb = v[b].reshape(N, HEADS, d).permute(1, 0, 2)
+        for fr in range(f):
+            qb = q[b * f + fr].reshape(N, HEADS, d).permute(1, 0, 2)
+            s = torch.softmax(torch.bmm(qb, kb.transpose(1, 2)) * (d ** -0.5), dim=-1)
+            out[b * f + fr] = torch.bmm(s, vb).permute(1, 0, 2).reshape(N, C)
+    return _lin(out, sd, p + "to_out.0.")
+
+
+def hooked(sd, p, x, ctx, controller, place):
+    """ptp_utils.py:196-221 (torch CPU fp32, global-max softmax, numpy oracle controller)."""
+    is_cross = ctx is not None
+    c = ctx if is_cross else x
+    q = O.heads_to_batch(_lin(x, sd, p + "to_q.").numpy(), HEADS)
+    k = O.heads_to_batch(_lin(c, sd, p + "to_k.").numpy(), HEADS)
+    v = O.heads_to_batch(_lin(c, sd, p + "to_v.").numpy(), HEADS)
+    sim = torch.bmm(torch.from_numpy(q), torch.from_numpy(k).transpose(1, 2)) * (q.shape[-1] ** -0.5)
+    e = torch.exp(sim - sim.max())
+    attn = (e / e.sum(-1, keepdim=True)).numpy()
+    if controller is not None:
+        attn = controller(attn, is_cross, place)
+    out = torch.bmm(torch.from_numpy(np.ascontiguousarray(attn)), torch.from_numpy(v)).numpy()
+    return _lin(torch.from_numpy(O.batch_to_heads(out, HEADS)), sd, p + "to_out.0.")
+
+
+def transformer(sd, p, x5, ctx, controller, place):
+    B, C, f, H, W = x5.shape
+    x = x5.permute(0, 2, 1, 3, 4).reshape(B * f, C, H, W)
+    res = x
+    h = F.group_norm(x, 32, sd[p + "norm.weight"], sd[p + "norm.bias"], 1e-6)
+    h = F.conv2d(h, sd[p + "proj_in.weight"], sd[p + "proj_in.bias"])
+    t = h.permute(0, 2, 3, 1).reshape(B * f, H * W, C)
+    q = p + "transformer_blocks.0."
+    t = frame_attention(sd, q + "attn1.", _ln(t, sd, q + "norm1."), f) + t
+    ctx_f = ctx.repeat_interleave(f, 0)                                   # attention.py:95
+    t = hooked(sd, q + "attn2.", _ln(t, sd, q + "norm2."), ctx_f, controller, place) + t
+    a, g = _lin(_ln(t, sd, q + "norm3."), sd, q + "ff.net.0.proj.").chunk(2, dim=-1)
+    t = _lin(a * F.gelu(g), sd, q + "ff.net.2.") + t
+    tt = t.reshape(B, f, H * W, C).permute(0, 2, 1, 3).reshape(B * H * W, f, C)   # '(b d) f c'
+    tt = hooked(sd, q + "attn_temp.", _ln(tt, sd, q + "norm_temp."), None, controller, place) + tt
+    t = tt.reshape(B, H * W, f, C).permute(0, 2, 1, 3).reshape(B * f, H * W, C)
+    h = t.reshape(B * f, H, W, C).permute(0, 3, 1, 2)
+    h = F.conv2d(h, sd[p + "proj_out.weight"], sd[p + "proj_out.bias"]) + res
+    return h.reshape(B, f, C, H, W).permute(0, 2, 1, 3, 4)
+
+
+def timestep_embedding(t: torch.Tensor, dim: int = 320) -> torch.Tensor:
+    half = dim // 2
+    freqs = torch.exp(-math.log(10000) * torch.arange(half, dtype=torch.float32) / half)
+    e = t[:, None].float() * freqs[None]
+    return torch.cat([torch.cos(e), torch.sin(e)], dim=-1)   # flip_sin_to_cos=True
+
+
+def unet_forward(sd: Dict[str, torch.Tensor], sample: torch.Tensor, timestep: int, ctx: torch.Tensor,
+                 controller=None, n_down: int = 4, layers: int = 2) -> torch.Tensor:
+    """sample (B, 4, f, H, W), ctx (B, 77, D) -> noise prediction (B, 4, f, H, W)."""
+    sd = {k: v.float().cpu() for k, v in sd.items()}
+    B = sample.shape[0]
+    t = torch.full((B,), int(timestep), dtype=torch.int64)
+    emb = _lin(F.silu(_lin(timestep_embedding(t, sd["conv_in.weight"].shape[0]), sd, "time_embedding.linear_1.")),
+               sd, "time_embedding.linear_2.")
+    x = _conv_frames(sample.float(), sd, "conv_in.")
+    skips = [x]
+    for i in range(n_down):
+        p = f"down_blocks.{i}."
+        for j in range(layers):
+            x = resnet(sd, p + f"resnets.{j}.", x, emb)
+            if (p + f"attentions.{j}.norm.weight") in sd:
+                x = transformer(sd, p + f"attentions.{j}.", x, ctx, controller, "down")
+            skips.append(x)
+        if (p + "downsamplers.0.conv.weight") in sd:
+            x = _conv_frames(x, sd, p + "downsamplers.0.conv.", stride=2)
+            skips.append(x)
+    x = resnet(sd, "mid_block.resnets.0.", x, emb)
+    x = transformer(sd, "mid_block.attentions.0.", x, ctx, controller, "mid")
+    x = resnet(sd, "mid_block.resnets.1.", x, emb)
+    for i in range(n_down):
+        p = f"up_blocks.{i}."
+        for j in range(layers + 1):
+            x = torch.cat([x, skips.pop()], dim=1)
+            x = resnet(sd, p + f"resnets.{j}.", x, emb)
+            if (p + f"attentions.{j}.norm.weight") in sd:
+                x = transformer(sd, p + f"attentions.{j}.", x, ctx, controller, "up")
+        if (p + "upsamplers.0.conv.weight") in sd:
+            B_, C_, f_, H_, W_ = x.shape
+            x = F.interpolate(x, scale_factor=(1.0, 2.0, 2.0), mode="nearest")
+            x = _conv_frames(x, sd, p + "upsamplers.0.conv.")
+    x = F.silu(F.group_norm(x, 32, sd["conv_norm_out.weight"], sd["conv_norm_out.bias"], 1e-5))
+    return _conv_frames(x, sd, "conv_out.")

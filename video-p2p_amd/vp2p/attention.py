@@ -1,0 +1,251 @@
+"""Attention modules of the video UNet and the drop-in ``register_attention_control``.
+
+``CrossAttention`` exposes the diffusers-0.11.1 attribute set the reference hook relies on
+(to_q / to_k / to_v / to_out[0], heads, scale, reshape_heads_to_batch_dim,
+reshape_batch_dim_to_heads; ptp_utils.py:189-208), so ``register_attention_control`` patches our
+modules and the reference's tuneavideo modules alike.  Its patched forward runs the hooked math
+of ptp_utils.py:196-221 on the HIP kernels:
+
+* cross  (attn2)    -> K2  ``vp2p_cross_attn_p2p_fwd``   (edit + LocalBlend reduction fused)
+* self   (attn_temp)-> K3  ``vp2p_temporal_attn_p2p_fwd`` (self-replace fused)
+* FrameAttention (attn1, never hooked in the reference: its class name differs,
+  ptp_utils.py:237) -> K1 ``vp2p_frame_attn_fwd``
+
+Projections stay on hipBLASLt GEMMs (``F.linear``); K/V of attn1 are projected for frame 0 only,
+K/V of attn2 once per batch row instead of once per frame, and attn_temp's q/k/v come from one GEMM
+against the concatenated weights -- all bit-identical to the reference's per-row projections.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .controllers import LayerCall
+
+
+def _cat_weight(module: nn.Module, names, cache_attr: str) -> torch.Tensor:
+    ws = [getattr(module, n).weight for n in names]
+    key = tuple((w.data_ptr(), w._version, w.dtype, w.device) for w in ws)
+    hit = getattr(module, cache_attr, None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    cat = torch.cat([w.detach() for w in ws], 0).contiguous()
+    object.__setattr__(module, cache_attr, (key, cat))
+    return cat
+
+
+class CrossAttention(nn.Module):
+    """diffusers 0.11.1 ``CrossAttention`` parameter layout (bias-free q/k/v, to_out = [Linear,
+    Dropout]); forward = plain (un-hooked) attention on the HIP kernels."""
+
+    def __init__(self, query_dim: int, cross_attention_dim: Optional[int] = None, heads: int = 8,
+                 dim_head: int = 64, dropout: float = 0.0, bias: bool = False,
+                 upcast_attention: bool = False):
+        super().__init__()
+        inner = heads * dim_head
+        ctx = cross_attention_dim if cross_attention_dim is not None else query_dim
+        self.heads = heads
+        self.scale = dim_head ** -0.5
+        self.upcast_attention = upcast_attention
+        self.to_q = nn.Linear(query_dim, inner, bias=bias)
+        self.to_k = nn.Linear(ctx, inner, bias=bias)
+        self.to_v = nn.Linear(ctx, inner, bias=bias)
+        self.to_out = nn.ModuleList([nn.Linear(inner, query_dim), nn.Dropout(dropout)])
+
+    def reshape_heads_to_batch_dim(self, t):
+        b, n, dim = t.shape
+        h = self.heads
+        return t.reshape(b, n, h, dim // h).permute(0, 2, 1, 3).reshape(b * h, n, dim // h)
+
+    def reshape_batch_dim_to_heads(self, t):
+        bh, n, d = t.shape
+        h = self.heads
+        return t.reshape(bh // h, h, n, d).permute(0, 2, 1, 3).reshape(bh // h, n, h * d)
+
+    def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, video_length=None,
+                temporal_layout=None):
+        return hooked_attention(self, None, "none", hidden_states, encoder_hidden_states, attention_mask,
+                                video_length, temporal_layout)
+
+
+class FrameAttention(CrossAttention):
+    """Sparse-causal frame attention with first-frame K/V (attention.py:273-329) on K1."""
+
+    def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, video_length=None):
+        if attention_mask is not None:
+            raise NotImplementedError("FrameAttention: attention_mask (never passed by the UNet)")
+        if encoder_hidden_states is not None:
+            raise NotImplementedError("FrameAttention: only_cross_attention")
+        x = hidden_states
+        f = video_length
+        B = x.shape[0] // f
+        q = F.linear(x, self.to_q.weight, self.to_q.bias)
+        x0 = x.view(B, f, *x.shape[1:])[:, 0]
+        kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
+                      None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
+        C = q.shape[-1]
+        out = ops.frame_attention(q, kv[..., :C], kv[..., C:], f, self.heads, scale=self.scale)
+        return self.to_out[1](self.to_out[0](out))
+
+
+def _batch_frames(x, controller, video_length):
+    P = getattr(controller, "batch_size", 0) or 0
+    if video_length:
+        return x.shape[0] // video_length, video_length, P
+    if P and x.shape[0] % (2 * P) == 0:
+        return 2 * P, x.shape[0] // (2 * P), P
+    return x.shape[0], 1, 0
+
+
+def hooked_attention(module, controller, place, x, context=None, attention_mask=None, video_length=None,
+                     temporal_layout=None):
+    """The patched forward (ptp_utils.py:196-221) for ``controller`` on the HIP kernels."""
+    if attention_mask is not None:
+        raise NotImplementedError("attention_mask is not supported on the fused path "
+                                  "(the reference UNet never passes one, pipeline_tuneavideo.py:406)")
+    is_cross = context is not None
+    fused = controller is None or getattr(controller, "fused", False)
+    h = module.heads
+    to_out = module.to_out[0] if isinstance(module.to_out, nn.ModuleList) else module.to_out
+    dev = x.device
+
+    if is_cross:
+        B, f, P = _batch_frames(x, controller, video_length)
+        N = x.shape[1]
+        P = P if B == 2 * P else 0
+        # the context is repeated per frame (attention.py:95); project it once per batch row
+        ctx = context if context.shape[0] == B else context.reshape(B, f, *context.shape[1:])[:, 0]
+        q = F.linear(x, module.to_q.weight, module.to_q.bias)
+        k = F.linear(ctx, module.to_k.weight, module.to_k.bias).contiguous()
+        v = F.linear(ctx, module.to_v.weight, module.to_v.bias).contiguous()
+        call = controller.fused_begin(True, place, N, f) if (controller is not None and fused) else LayerCall()
+        probs = None
+        if call.store or not fused:
+            probs = torch.empty(B * f * h, N, k.shape[1], device=dev, dtype=torch.float32)
+        plan = None
+        lb = None
+        if fused and controller is not None and (call.edit or call.lb_acc):
+            plan = controller.plan(dev)
+            if call.lb_acc:
+                lb = controller.lb_buffer(f, dev)
+        out = ops.cross_attention_p2p(q, k, v, f, h, plan=plan, step=call.step, edit=call.edit, lb_acc=lb,
+                                      probs_out=probs, prompts=P, scale=module.scale)
+        if not fused:
+            attn = controller(probs, True, place)
+            out = _pv(module, attn, v, B, f)
+        elif controller is not None:
+            controller.fused_end(True, place, call, probs)
+        return to_out(out)
+
+    # self attention on the hooked path = temporal attention (attn_temp)
+    C = module.to_q.weight.shape[0]
+    w = _cat_weight(module, ("to_q", "to_k", "to_v"), "_wqkv")
+    bias = None
+    if module.to_q.bias is not None:
+        bias = torch.cat([module.to_q.bias, module.to_k.bias, module.to_v.bias])
+    qkv = F.linear(x, w, bias)
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    if temporal_layout == "bf":
+        f = video_length
+        B = x.shape[0] // f
+        N = x.shape[1]
+    else:  # the reference's '(b d) f c' tensor
+        f = x.shape[1]
+        P0 = getattr(controller, "batch_size", 0) or 0
+        B = 2 * P0 if (P0 and x.shape[0] % (2 * P0) == 0) else 1
+        N = x.shape[0] // B
+    P = getattr(controller, "batch_size", 0) or 0
+    P = P if B == 2 * P else 0
+    call = controller.fused_begin(False, place, f, f) if (controller is not None and fused) else LayerCall()
+    probs = None
+    if call.store or not fused:
+        probs = torch.empty(B * N * h, f, f, device=dev, dtype=torch.float32)
+    replace = bool(call.self_replace) and P > 0
+    if temporal_layout == "bf":
+        out = ops.temporal_attention_p2p(q, k, v, f, h, prompts=P, self_replace=replace, probs_out=probs,
+                                         scale=module.scale)
+    else:
+        out = ops.temporal_attention_p2p_bd(q, k, v, B, h, prompts=P, self_replace=replace, probs_out=probs,
+                                            scale=module.scale)
+    if not fused:
+        attn = controller(probs, False, place)
+        out = _pv_temporal(module, attn, v, B, f, N, temporal_layout == "bf")
+    elif controller is not None:
+        controller.fused_end(False, place, call, probs)
+    return to_out(out)
+
+
+def _pv(module, attn, v, B, f):
+    """attn @ v for a foreign controller's edited maps: (B*f*h, N, M) x (B, M, C)."""
+    h = module.heads
+    vb = module.reshape_heads_to_batch_dim(v.repeat_interleave(f, 0)).to(attn.dtype)
+    out = torch.bmm(attn, vb)
+    return module.reshape_batch_dim_to_heads(out).to(v.dtype)
+
+
+def _pv_temporal(module, attn, v, B, f, N, bf_layout):
+    h = module.heads
+    C = v.shape[-1]
+    if bf_layout:
+        vv = v.reshape(B, f, N, C).permute(0, 2, 1, 3).reshape(B * N, f, C)
+    else:
+        vv = v
+    out = torch.bmm(attn, module.reshape_heads_to_batch_dim(vv).to(attn.dtype))
+    out = module.reshape_batch_dim_to_heads(out).to(v.dtype)
+    if bf_layout:
+        out = out.reshape(B, N, f, C).permute(0, 2, 1, 3).reshape(B * f, N, C)
+    return out
+
+
+class DummyController:
+    """ptp_utils.py:225-234."""
+
+    fused = True
+
+    def __call__(self, *args):
+        return args[0]
+
+    def __init__(self):
+        self.num_att_layers = 0
+
+    def fused_begin(self, *a):
+        return LayerCall()
+
+    def fused_end(self, *a):
+        return None
+
+
+def register_attention_control(model, controller):
+    """ptp_utils.py:188-255: patch every module whose class is named ``CrossAttention`` under the
+    UNet's down*/up*/mid* children; set ``controller.num_att_layers``."""
+    ctrl = DummyController() if controller is None else controller
+
+    def make_forward(net, place):
+        def forward(x, encoder_hidden_states=None, attention_mask=None, video_length=None,
+                    temporal_layout=None):
+            return hooked_attention(net, None if controller is None else ctrl, place, x,
+                                    encoder_hidden_states, attention_mask, video_length, temporal_layout)
+        return forward
+
+    def walk(net, count, place):
+        if net.__class__.__name__ == "CrossAttention":
+            net.forward = make_forward(net, place)
+            return count + 1
+        for child in net.children():
+            count = walk(child, count, place)
+        return count
+
+    total = 0
+    for name, child in model.unet.named_children():
+        if "down" in name:
+            total += walk(child, 0, "down")
+        elif "up" in name:
+            total += walk(child, 0, "up")
+        elif "mid" in name:
+            total += walk(child, 0, "mid")
+    ctrl.num_att_layers = total
+    return ctrl

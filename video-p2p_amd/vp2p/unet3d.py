@@ -1,0 +1,380 @@
+"""UNet3DConditionModel of Tune-A-Video (tuneavideo/models/unet.py, unet_blocks.py, resnet.py,
+attention.py) without diffusers: same module tree and state-dict keys, so tuneavideo checkpoints
+load and ``register_attention_control`` finds the same 32 hooked layers in the same call order.
+
+Layout: activations stay ``(b f) c h w`` in channels-last memory, i.e. physically
+``(b f) h w c``.  That is the inflated-conv input (resnet.py:11-19) with no rearrange, and its
+token view ``(b f) (h w) c`` is what the transformer blocks consume (attention.py:94-108), also
+without a copy.  The 5-D GroupNorms of the reference (statistics over c/G x f x h x w,
+resnet.py:142,158; unet.py:206) are computed on that layout directly.
+
+Only the attention layers run hand-written HIP kernels here; convolutions / GEMMs / norms use
+PyTorch-ROCm (MIOpen / hipBLASLt) -- SURVEY §8(f) rank 1 is the next row to move.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .attention import CrossAttention, FrameAttention
+
+
+@dataclass
+class UNet3DConditionOutput:
+    sample: torch.Tensor
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bool = False) -> torch.Tensor:
+    """GroupNorm whose statistics span ``frames`` consecutive samples of a ``(b f) c h w``
+    channels-last tensor (frames=1: the per-frame GroupNorm of Transformer3DModel.norm)."""
+    Bf, C, H, W = x.shape
+    B = Bf // frames
+    G = norm.num_groups
+    xv = x.permute(0, 2, 3, 1).reshape(B, frames * H * W, G, C // G)
+    xf = xv.float()
+    var, mean = torch.var_mean(xf, dim=(1, 3), keepdim=True, unbiased=False)
+    y = (xf - mean) * torch.rsqrt(var + norm.eps)
+    y = y.reshape(Bf, H, W, C)
+    if norm.affine:
+        y = y * norm.weight.float() + norm.bias.float()
+    if silu:
+        y = F.silu(y)
+    return y.to(x.dtype).permute(0, 3, 1, 2)
+
+
+def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0) -> torch.Tensor:
+    """diffusers get_timestep_embedding (max_period 10000)."""
+    half = dim // 2
+    exponent = -math.log(10000) * torch.arange(half, dtype=torch.float32, device=t.device) / (half - shift)
+    emb = t[:, None].float() * torch.exp(exponent)[None, :]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+    return emb
+
+
+class Timesteps(nn.Module):
+    def __init__(self, num_channels: int, flip_sin_to_cos: bool, downscale_freq_shift: float):
+        super().__init__()
+        self.num_channels, self.flip, self.shift = num_channels, flip_sin_to_cos, downscale_freq_shift
+
+    def forward(self, t):
+        return timestep_embedding(t, self.num_channels, self.flip, self.shift)
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, in_channels: int, time_embed_dim: int):
+        super().__init__()
+        self.linear_1 = nn.Linear(in_channels, time_embed_dim)
+        self.act = nn.SiLU()
+        self.linear_2 = nn.Linear(time_embed_dim, time_embed_dim)
+
+    def forward(self, x):
+        return self.linear_2(self.act(self.linear_1(x)))
+
+
+class InflatedConv3d(nn.Conv2d):
+    """Per-frame Conv2d; input/output already '(b f) c h w'."""
+
+
+class ResnetBlock3D(nn.Module):
+    def __init__(self, in_channels, out_channels, temb_channels=1280, groups=32, eps=1e-5,
+                 output_scale_factor=1.0, dropout=0.0):
+        super().__init__()
+        self.norm1 = nn.GroupNorm(groups, in_channels, eps=eps, affine=True)
+        self.conv1 = InflatedConv3d(in_channels, out_channels, 3, 1, 1)
+        self.time_emb_proj = nn.Linear(temb_channels, out_channels)
+        self.norm2 = nn.GroupNorm(groups, out_channels, eps=eps, affine=True)
+        self.dropout = nn.Dropout(dropout)
+        self.conv2 = InflatedConv3d(out_channels, out_channels, 3, 1, 1)
+        self.output_scale_factor = output_scale_factor
+        self.conv_shortcut = (InflatedConv3d(in_channels, out_channels, 1, 1, 0)
+                              if in_channels != out_channels else None)
+
+    def forward(self, x, temb, frames):
+        h = self.conv1(group_norm_frames(x, self.norm1, frames, silu=True))
+        t = self.time_emb_proj(F.silu(temb)).repeat_interleave(frames, 0)
+        h = h + t[:, :, None, None].to(h.dtype)
+        h = self.conv2(self.dropout(group_norm_frames(h, self.norm2, frames, silu=True)))
+        sc = x if self.conv_shortcut is None else self.conv_shortcut(x)
+        out = sc + h
+        if self.output_scale_factor != 1.0:
+            out = out / self.output_scale_factor
+        return out
+
+
+class GEGLU(nn.Module):
+    def __init__(self, dim_in, dim_out):
+        super().__init__()
+        self.proj = nn.Linear(dim_in, dim_out * 2)
+
+    def forward(self, x):
+        a, g = self.proj(x).chunk(2, dim=-1)
+        return a * F.gelu(g)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim, mult=4, dropout=0.0):
+        super().__init__()
+        inner = dim * mult
+        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(dropout), nn.Linear(inner, dim)])
+
+    def forward(self, x):
+        for m in self.net:
+            x = m(x)
+        return x
+
+
+class BasicTransformerBlock(nn.Module):
+    """attention.py:140-270: frame attn -> cross attn -> FF -> temporal attn, pre-LayerNorm."""
+
+    def __init__(self, dim, heads, dim_head, cross_attention_dim):
+        super().__init__()
+        self.attn1 = FrameAttention(dim, heads=heads, dim_head=dim_head)
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn2 = CrossAttention(dim, cross_attention_dim, heads=heads, dim_head=dim_head)
+        self.norm2 = nn.LayerNorm(dim)
+        self.ff = FeedForward(dim)
+        self.norm3 = nn.LayerNorm(dim)
+        self.attn_temp = CrossAttention(dim, heads=heads, dim_head=dim_head)
+        self.norm_temp = nn.LayerNorm(dim)
+
+    def forward(self, x, context, frames):
+        x = self.attn1(self.norm1(x), video_length=frames) + x
+        x = self.attn2(self.norm2(x), encoder_hidden_states=context, video_length=frames) + x
+        x = self.ff(self.norm3(x)) + x
+        x = self.attn_temp(self.norm_temp(x), video_length=frames, temporal_layout="bf") + x
+        return x
+
+
+class Transformer3DModel(nn.Module):
+    def __init__(self, heads, dim_head, in_channels, cross_attention_dim, groups=32):
+        super().__init__()
+        inner = heads * dim_head
+        self.norm = nn.GroupNorm(groups, in_channels, eps=1e-6, affine=True)
+        self.proj_in = nn.Conv2d(in_channels, inner, 1)
+        self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(inner, heads, dim_head, cross_attention_dim)])
+        self.proj_out = nn.Conv2d(inner, in_channels, 1)
+
+    def forward(self, x, context, frames):
+        Bf, C, H, W = x.shape
+        h = group_norm_frames(x, self.norm, 1)
+        tok = h.permute(0, 2, 3, 1).reshape(Bf, H * W, C)
+        tok = F.linear(tok, self.proj_in.weight.view(self.proj_in.out_channels, -1), self.proj_in.bias)
+        for blk in self.transformer_blocks:
+            tok = blk(tok, context, frames)
+        tok = F.linear(tok, self.proj_out.weight.view(self.proj_out.out_channels, -1), self.proj_out.bias)
+        return tok.reshape(Bf, H, W, C).permute(0, 3, 1, 2) + x
+
+
+class Downsample3D(nn.Module):
+    def __init__(self, channels):
+        super().__init__()
+        self.conv = InflatedConv3d(channels, channels, 3, stride=2, padding=1)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class Upsample3D(nn.Module):
+    def __init__(self, channels):
+        super().__init__()
+        self.conv = InflatedConv3d(channels, channels, 3, padding=1)
+
+    def forward(self, x, size=None):
+        if size is None:
+            x = F.interpolate(x, scale_factor=2.0, mode="nearest")
+        else:
+            x = F.interpolate(x, size=size, mode="nearest")
+        return self.conv(x.contiguous(memory_format=torch.channels_last))
+
+
+class CrossAttnDownBlock3D(nn.Module):
+    def __init__(self, cin, cout, temb, heads, ctx_dim, add_downsample, layers=2, eps=1e-5):
+        super().__init__()
+        self.has_cross_attention = True
+        self.resnets = nn.ModuleList([ResnetBlock3D(cin if i == 0 else cout, cout, temb, eps=eps) for i in range(layers)])
+        self.attentions = nn.ModuleList([Transformer3DModel(heads, cout // heads, cout, ctx_dim) for _ in range(layers)])
+        self.downsamplers = nn.ModuleList([Downsample3D(cout)]) if add_downsample else None
+
+    def forward(self, x, temb, ctx, frames):
+        outs = ()
+        for r, a in zip(self.resnets, self.attentions):
+            x = a(r(x, temb, frames), ctx, frames)
+            outs += (x,)
+        if self.downsamplers is not None:
+            x = self.downsamplers[0](x)
+            outs += (x,)
+        return x, outs
+
+
+class DownBlock3D(nn.Module):
+    def __init__(self, cin, cout, temb, add_downsample, layers=2, eps=1e-5):
+        super().__init__()
+        self.has_cross_attention = False
+        self.resnets = nn.ModuleList([ResnetBlock3D(cin if i == 0 else cout, cout, temb, eps=eps) for i in range(layers)])
+        self.downsamplers = nn.ModuleList([Downsample3D(cout)]) if add_downsample else None
+
+    def forward(self, x, temb, ctx, frames):
+        outs = ()
+        for r in self.resnets:
+            x = r(x, temb, frames)
+            outs += (x,)
+        if self.downsamplers is not None:
+            x = self.downsamplers[0](x)
+            outs += (x,)
+        return x, outs
+
+
+class UNetMidBlock3DCrossAttn(nn.Module):
+    def __init__(self, c, temb, heads, ctx_dim, eps=1e-5, output_scale_factor=1.0):
+        super().__init__()
+        self.has_cross_attention = True
+        self.resnets = nn.ModuleList([ResnetBlock3D(c, c, temb, eps=eps, output_scale_factor=output_scale_factor)
+                                      for _ in range(2)])
+        self.attentions = nn.ModuleList([Transformer3DModel(heads, c // heads, c, ctx_dim)])
+
+    def forward(self, x, temb, ctx, frames):
+        x = self.resnets[0](x, temb, frames)
+        for a, r in zip(self.attentions, self.resnets[1:]):
+            x = r(a(x, ctx, frames), temb, frames)
+        return x
+
+
+class _UpBlock(nn.Module):
+    def _build(self, cin, cout, prev, temb, add_upsample, layers, eps):
+        self.resnets = nn.ModuleList([
+            ResnetBlock3D((prev if i == 0 else cout) + (cin if i == layers - 1 else cout), cout, temb, eps=eps)
+            for i in range(layers)])
+        self.upsamplers = nn.ModuleList([Upsample3D(cout)]) if add_upsample else None
+
+    def forward(self, x, skips, temb, ctx, frames, upsample_size=None):
+        for i, r in enumerate(self.resnets):
+            x = torch.cat([x, skips[-1 - i]], dim=1)
+            x = r(x, temb, frames)
+            if self.attentions is not None:
+                x = self.attentions[i](x, ctx, frames)
+        if self.upsamplers is not None:
+            x = self.upsamplers[0](x, upsample_size)
+        return x
+
+
+class CrossAttnUpBlock3D(_UpBlock):
+    def __init__(self, cin, cout, prev, temb, heads, ctx_dim, add_upsample, layers=3, eps=1e-5):
+        super().__init__()
+        self.has_cross_attention = True
+        self._build(cin, cout, prev, temb, add_upsample, layers, eps)
+        self.attentions = nn.ModuleList([Transformer3DModel(heads, cout // heads, cout, ctx_dim) for _ in range(layers)])
+
+
+class UpBlock3D(_UpBlock):
+    def __init__(self, cin, cout, prev, temb, add_upsample, layers=3, eps=1e-5):
+        super().__init__()
+        self.has_cross_attention = False
+        self._build(cin, cout, prev, temb, add_upsample, layers, eps)
+        self.attentions = None
+
+
+class UNet3DConditionModel(nn.Module):
+    """unet.py:38-414 with SD-1.5 geometry by default (cross_attention_dim 768, 8 heads)."""
+
+    def __init__(self, in_channels=4, out_channels=4, block_out_channels=(320, 640, 1280, 1280),
+                 layers_per_block=2, cross_attention_dim=768, attention_head_dim=8, norm_num_groups=32,
+                 norm_eps=1e-5, flip_sin_to_cos=True, freq_shift=0, sample_size=64):
+        super().__init__()
+        self.in_channels = in_channels
+        self.sample_size = sample_size
+        c0 = block_out_channels[0]
+        temb = c0 * 4
+        self.conv_in = InflatedConv3d(in_channels, c0, 3, padding=1)
+        self.time_proj = Timesteps(c0, flip_sin_to_cos, freq_shift)
+        self.time_embedding = TimestepEmbedding(c0, temb)
+        heads = attention_head_dim
+        self.down_blocks = nn.ModuleList()
+        cout = c0
+        n = len(block_out_channels)
+        for i, c in enumerate(block_out_channels):
+            cin, cout = cout, c
+            last = i == n - 1
+            if i < n - 1:
+                self.down_blocks.append(CrossAttnDownBlock3D(cin, cout, temb, heads, cross_attention_dim,
+                                                             not last, layers_per_block, norm_eps))
+            else:
+                self.down_blocks.append(DownBlock3D(cin, cout, temb, not last, layers_per_block, norm_eps))
+        self.mid_block = UNetMidBlock3DCrossAttn(block_out_channels[-1], temb, heads, cross_attention_dim, norm_eps)
+        self.up_blocks = nn.ModuleList()
+        rev = list(reversed(block_out_channels))
+        cout = rev[0]
+        for i in range(n):
+            prev, cout = cout, rev[i]
+            cin = rev[min(i + 1, n - 1)]
+            last = i == n - 1
+            if i == 0:
+                self.up_blocks.append(UpBlock3D(cin, cout, prev, temb, not last, layers_per_block + 1, norm_eps))
+            else:
+                self.up_blocks.append(CrossAttnUpBlock3D(cin, cout, prev, temb, heads, cross_attention_dim,
+                                                         not last, layers_per_block + 1, norm_eps))
+        self.conv_norm_out = nn.GroupNorm(norm_num_groups, c0, eps=norm_eps)
+        self.conv_act = nn.SiLU()
+        self.conv_out = InflatedConv3d(c0, out_channels, 3, padding=1)
+
+    @property
+    def dtype(self):
+        return self.conv_in.weight.dtype
+
+    def forward(self, sample: torch.Tensor, timestep, encoder_hidden_states: torch.Tensor,
+                return_dict: bool = True):
+        B, Cin, f, H, W = sample.shape
+        t = timestep
+        if not torch.is_tensor(t):
+            t = torch.tensor([t], dtype=torch.int64, device=sample.device)
+        elif t.dim() == 0:
+            t = t[None].to(sample.device)
+        t = t.expand(B)
+        emb = self.time_embedding(self.time_proj(t).to(self.dtype))
+        ctx = encoder_hidden_states.to(self.dtype)
+        x = sample.to(self.dtype).permute(0, 2, 1, 3, 4).reshape(B * f, Cin, H, W)
+        x = self.conv_in(x.contiguous(memory_format=torch.channels_last))
+        skips = (x,)
+        for blk in self.down_blocks:
+            x, res = blk(x, emb, ctx, f)
+            skips += res
+        x = self.mid_block(x, emb, ctx, f)
+        up_factor = 2 ** (len(self.up_blocks) - 1)
+        forward_size = any(s % up_factor for s in (H, W))
+        for i, blk in enumerate(self.up_blocks):
+            k = len(blk.resnets)
+            res, skips = skips[-k:], skips[:-k]
+            size = skips[-1].shape[2:] if (forward_size and i < len(self.up_blocks) - 1) else None
+            x = blk(x, res, emb, ctx, f, size)
+        x = self.conv_out(group_norm_frames(x, self.conv_norm_out, f, silu=True))
+        out = x.reshape(B, f, -1, H, W).permute(0, 2, 1, 3, 4)
+        if not return_dict:
+            return (out,)
+        return UNet3DConditionOutput(sample=out)
+
+
+def init_random_(model: nn.Module, seed: int = 0, std: float = 0.02) -> nn.Module:
+    """Synthetic weights for benchmarking: conv/linear N(0, std), biases 0, norms
+    (1, 0).  attn_temp.to_out is NOT zeroed (the reference zero-inits it, attention.py:202, which
+    would disable the temporal path)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, (nn.Linear, nn.Conv2d)):
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) * std)
+                if m.bias is not None:
+                    m.bias.zero_()
+            elif isinstance(m, (nn.GroupNorm, nn.LayerNorm)):
+                if m.weight is not None:
+                    m.weight.fill_(1.0)
+                    m.bias.zero_()
+    return model
