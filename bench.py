@@ -86,7 +86,7 @@ class K1Timer:
         achieved = flops / avg_s / 1e12
         return {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": None,
-                "kernel": "vp2p::frame_attn_kernel<bf16,40> (res-64 FrameAttention)",
+                "kernel": "vp2p::frame_attn_kernel_x2<40> (res-64 FrameAttention, bf16)",
                 "launches": len(ms), "avg_ms": round(sum(ms) / len(ms), 4),
                 "flops_per_launch": flops}
 

@@ -8,16 +8,34 @@
 // MI355X design:
 //  * K/V are only ever the B*h distinct frame-0 tensors; the f*HW queries of one (b, head) form one
 //    long query axis, so a workgroup = 128 query rows (4 waves x 32) of one (b, head) streams
-//    frame-0 K/V tiles of 64 keys through LDS, and the grid is XCD-remapped so the workgroups of one
-//    (b, head) share an L2.
+//    frame-0 K/V tiles through LDS, and the grid is XCD-remapped so the workgroups of one (b, head)
+//    share an L2.
 //  * swapped 32x32 MFMA tiles (common.hpp): softmax is lane-local, P never leaves registers,
 //    V is read transposed from its row-major LDS image with ds_read_b64_tr_b16.
-//  * online softmax in the log2 domain (one v_fma + v_exp per score), next K/V tile prefetched into
-//    registers while the current one is consumed (issue early / write late).
+//  * the kernel is VALU-bound at d = 40 (7 MFMAs per 32x32 block against 16 scores per lane), so the
+//    per-score VALU work is cut to max3 + fma + exp2 + cvt:
+//      - scores stay unscaled; p = exp2(s * c - m) is one v_fma + one v_exp,
+//      - the row sum rides in the MFMA: a spare row of the padded V^T (d = 40 -> 64 rows) is all
+//        ones, so O^T's row `D` accumulates sum_k P (rescaled together with O),
+//      - lazy rescale: m only moves when the block max exceeds it by > kRescaleThr (log2 units),
+//        so O is rarely touched; P <= 2^kRescaleThr in between (bf16-safe, fp32 accumulators),
+//      - masking only on the ragged last tile.
+//  * next K/V tile prefetched into registers while the current one is consumed
+//    (issue early / write late); two barriers per 128-key tile.
+//  * bf16, d <= 64 (the res-64 layers, 88% of the FLOPs): frame_attn_kernel_x2 gives every wave
+//    64 query rows as two independent 32-row sets sharing each K/V fragment read (half the LDS
+//    traffic per query, two independent MFMA/VALU chains per wave): +5% over one set per wave in
+//    an interleaved A/B (profiles/r01_k1_ab.txt).
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "common.hpp"
 #include "vp2p.h"
 
 namespace vp2p {
+
+constexpr float kRescaleThr = 8.0f;
 
 template <typename T, int D>
 struct FrameCfg {
@@ -27,7 +45,10 @@ struct FrameCfg {
   static constexpr int KS = DP / KD;
   static constexpr int DV = round_up(D, 32);
   static constexpr int NT = DV / 32;
-  static constexpr int KT = 64;                                  // keys per LDS tile
+  static constexpr bool ONES = D < DV;                           // spare V^T row carries the row sum
+  static constexpr int KT = (BF && D <= 80) ? 128 : 64;          // keys per LDS tile
+  static constexpr int NB = D <= 80 ? 2 : 1;                     // 32-key score blocks in flight
+  static constexpr int SUBK = 32 * NB;
   static constexpr int EPC = 16 / (int)sizeof(T);                // elements per 16-byte chunk
   static constexpr int CPR = D / EPC;                            // chunks per K/V row
   static constexpr int NCH = (KT * CPR + 255) / 256;             // chunks per thread per tile
@@ -42,6 +63,9 @@ struct FrameCfg {
   static constexpr int KROW = BF ? DP + 8 : DP + 1;
   static constexpr int VROW = BF ? vrow_bf16() : DV;
   static constexpr int LDS_BYTES = (KT * KROW + KT * VROW) * (int)sizeof(T);
+  // accumulator slot of O^T row D (the ones row): tile, register, lane half
+  static constexpr int ONE_T = D / 32, ONE_L = D % 32;
+  static constexpr int ONE_H = (ONE_L >> 2) & 1, ONE_I = (ONE_L & 3) + 4 * (ONE_L >> 3);
 };
 
 template <typename T, int D>
@@ -69,8 +93,12 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
 #pragma unroll
   for (int s = 0; s < C::KS; ++s) qf[s] = qv ? M::row_frag(qrow, s, h, D) : M::zero();
 
-  // zero the LDS image once: the padding columns (D..DP, D..DV) are never written again
+  // LDS image: zero once (padding columns are never rewritten); the ones column of V
   for (int i = tid; i < C::LDS_BYTES / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0, 0, 0, 0};
+  if constexpr (C::ONES) {
+    __syncthreads();
+    for (int k = tid; k < C::KT; k += 256) Vs[k * C::VROW + D] = (T)1.0f;
+  }
 
   const T* kbase = static_cast<const T*>(a.k) + b * a.k_sb + head * D;
   const T* vbase = static_cast<const T*>(a.v) + b * a.v_sb + head * D;
@@ -110,71 +138,112 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
   };
 
   const float cs = a.scale * kLog2e;
-  float m = kNegInf, lsum = 0.f;
+  float m = kNegInf;            // running max of s*cs (log2 units), shared by lanes r and r+32
+  float lsum = 0.f;             // only without the ones row
   f32x16 o[C::NT];
 #pragma unroll
   for (int t = 0; t < C::NT; ++t) o[t] = zero16();
 
+  // one K/V tile: QK^T, online softmax, PV.  MASKED only for the ragged last tile, so the hot loop
+  // carries no per-score key-bound compare/select.
+  auto compute_tile = [&](int kt, auto masked_tag) {
+    constexpr bool MASKED = decltype(masked_tag)::value;
+  #pragma unroll
+      for (int sub = 0; sub < C::KT / C::SUBK; ++sub) {
+        const int key0 = sub * C::SUBK;
+        if (MASKED && kt + key0 >= Nk) break;
+        f32x16 sc[C::NB];
+  #pragma unroll
+        for (int nb = 0; nb < C::NB; ++nb) sc[nb] = zero16();
+  #pragma unroll
+        for (int si = 0; si < C::KS; ++si) {
+  #pragma unroll
+          for (int nb = 0; nb < C::NB; ++nb) {
+            const T* krow = Ks + (key0 + 32 * nb + r) * C::KROW;
+            typename M::frag af;
+            if constexpr (C::BF) af = *reinterpret_cast<const bf16x8*>(krow + 16 * si + 8 * h);
+            else af = krow[2 * si + h];
+            sc[nb] = M::mma(af, qf[si], sc[nb]);
+          }
+        }
+        if constexpr (MASKED) {
+  #pragma unroll
+          for (int nb = 0; nb < C::NB; ++nb)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (kt + key0 + 32 * nb + acc_row(i, h) >= Nk) sc[nb][i] = kNegInf;
+        }
+        float mx = sc[0][0];
+  #pragma unroll
+        for (int nb = 0; nb < C::NB; ++nb)
+  #pragma unroll
+          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[nb][i]);
+        mx = fmaxf(mx, xhalf(mx)) * cs;
+        if (__any(mx > m + kRescaleThr)) {
+          const float mn = fmaxf(m, mx);
+          const float alpha = fast_exp2(m - mn);
+          m = mn;
+  #pragma unroll
+          for (int t = 0; t < C::NT; ++t)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
+          if constexpr (!C::ONES) lsum *= alpha;
+        }
+        const float nm = -m;
+  #pragma unroll
+        for (int nb = 0; nb < C::NB; ++nb)
+  #pragma unroll
+          for (int i = 0; i < 16; ++i) sc[nb][i] = fast_exp2(__builtin_fmaf(sc[nb][i], cs, nm));
+        if constexpr (!C::ONES) {
+  #pragma unroll
+          for (int nb = 0; nb < C::NB; ++nb)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) lsum += sc[nb][i];
+        }
+  #pragma unroll
+        for (int nb = 0; nb < C::NB; ++nb) {
+  #pragma unroll
+          for (int sp = 0; sp < M::PV_STEPS; ++sp) {
+            const typename M::frag pf = M::p_frag(sc[nb], sp);
+  #pragma unroll
+            for (int t = 0; t < C::NT; ++t) {
+              typename M::frag vf;
+              if constexpr (C::BF) vf = vt_frag_lds<C::VROW>(Vs, key0 + 32 * nb, sp, t);
+              else vf = Vs[(key0 + 32 * nb + f32_pv_key(sp, h)) * C::VROW + 32 * t + r];
+              o[t] = M::mma(vf, pf, o[t]);
+            }
+          }
+        }
+      }
+
+  };
+
   load_tile(0);
-  for (int kt = 0; kt < Nk; kt += C::KT) {
+  int kt = 0;
+  for (; kt + C::KT <= Nk; kt += C::KT) {
     __syncthreads();
     store_tile();
     __syncthreads();
     if (kt + C::KT < Nk) load_tile(kt + C::KT);
-
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-      const int key0 = blk * 32;
-      if (kt + key0 >= Nk) break;
-      f32x16 s = zero16();
-      const T* krow = Ks + (key0 + r) * C::KROW;
-#pragma unroll
-      for (int si = 0; si < C::KS; ++si) {
-        typename M::frag af;
-        if constexpr (C::BF) af = *reinterpret_cast<const bf16x8*>(krow + 16 * si + 8 * h);
-        else af = krow[2 * si + h];
-        s = M::mma(af, qf[si], s);
-      }
-      float mx = kNegInf;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float v = (kt + key0 + acc_row(i, h) < Nk) ? s[i] * cs : kNegInf;
-        s[i] = v;
-        mx = fmaxf(mx, v);
-      }
-      mx = fmaxf(mx, xhalf(mx));
-      const float mn = fmaxf(m, mx);
-      const float alpha = fast_exp2(m - mn);
-      float rs = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = fast_exp2(s[i] - mn);
-        s[i] = p;
-        rs += p;
-      }
-      rs += xhalf(rs);
-      lsum = lsum * alpha + rs;
-      m = mn;
-#pragma unroll
-      for (int t = 0; t < C::NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
-#pragma unroll
-      for (int sp = 0; sp < M::PV_STEPS; ++sp) {
-        const typename M::frag pf = M::p_frag(s, sp);
-#pragma unroll
-        for (int t = 0; t < C::NT; ++t) {
-          typename M::frag vf;
-          if constexpr (C::BF) vf = vt_frag_lds<C::VROW>(Vs, key0, sp, t);
-          else vf = Vs[(key0 + f32_pv_key(sp, h)) * C::VROW + 32 * t + r];
-          o[t] = M::mma(vf, pf, o[t]);
-        }
-      }
-    }
+    compute_tile(kt, std::false_type{});
+  }
+  if (kt < Nk) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    compute_tile(kt, std::true_type{});
   }
 
+  float lrow;
+  if constexpr (C::ONES) {
+    const float mine = o[C::ONE_T][C::ONE_I];
+    const float other = xhalf(mine);
+    lrow = (h == C::ONE_H) ? mine : other;
+  } else {
+    lrow = lsum + xhalf(lsum);
+  }
   if (qv) {
-    const float inv = 1.f / lsum;
+    const float inv = 1.f / lrow;
     T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
 #pragma unroll
     for (int t = 0; t < C::NT; ++t) {
@@ -199,10 +268,194 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
   }
 }
 
+// Variant with 64 query rows per wave: two independent 32-row sets share every K/V fragment read
+// (half the LDS traffic per query) and give the scheduler two independent MFMA/VALU chains.
+// bf16, head dims with a spare ones row (d = 32 excluded), d <= 64.
+template <int D>
+__global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2(const vp2p_frame_attn_args a) {
+  using T = bf16;
+  using M = Mfma<T>;
+  using C = FrameCfg<T, D>;
+  static_assert(C::ONES && D <= 64, "x2 variant: bf16, spare ones row");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Ks = reinterpret_cast<T*>(smem);
+  T* Vs = Ks + C::KT * C::KROW;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int FQ = a.frames * a.tokens_q;
+  const int qblocks = (FQ + 255) >> 8;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = bid / qblocks, qb = bid - bh * qblocks;
+  const int b = bh / a.heads, head = bh - b * a.heads;
+  const int Nk = a.tokens_kv;
+
+  int qi[2], fr[2], pos[2];
+  bool qv[2];
+  bf16x8 qf[2][C::KS];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    qi[st] = qb * 256 + w * 64 + st * 32 + r;
+    qv[st] = qi[st] < FQ;
+    fr[st] = qv[st] ? qi[st] / a.tokens_q : 0;
+    pos[st] = qv[st] ? qi[st] - fr[st] * a.tokens_q : 0;
+    const T* qrow = static_cast<const T*>(a.q) + b * a.q_sb + fr[st] * a.q_sf + pos[st] * a.q_sn + head * D;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[st][s] = qv[st] ? M::row_frag(qrow, s, h, D) : M::zero();
+  }
+  for (int i = tid; i < C::LDS_BYTES / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0, 0, 0, 0};
+  __syncthreads();
+  for (int k = tid; k < C::KT; k += 256) Vs[k * C::VROW + D] = (T)1.0f;
+
+  const T* kbase = static_cast<const T*>(a.k) + b * a.k_sb + head * D;
+  const T* vbase = static_cast<const T*>(a.v) + b * a.v_sb + head * D;
+  u32x4 kreg[C::NCH], vreg[C::NCH];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < C::NCH; ++i) {
+      const int c = tid + i * 256;
+      const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
+      const int key = kt + row;
+      if (c < C::KT * C::CPR && key < Nk) {
+        kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)key * a.k_sn + col);
+        vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (int64_t)key * a.v_sn + col);
+      } else {
+        kreg[i] = u32x4{0, 0, 0, 0};
+        vreg[i] = u32x4{0, 0, 0, 0};
+      }
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < C::NCH; ++i) {
+      const int c = tid + i * 256;
+      if (c < C::KT * C::CPR) {
+        const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
+        *reinterpret_cast<u32x4*>(Ks + row * C::KROW + col) = kreg[i];
+        *reinterpret_cast<u32x4*>(Vs + row * C::VROW + col) = vreg[i];
+      }
+    }
+  };
+
+  const float cs = a.scale * kLog2e;
+  float m[2] = {kNegInf, kNegInf};
+  f32x16 o[2][C::NT];
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t) o[st][t] = zero16();
+
+  auto compute_tile = [&](int kt, auto masked_tag) {
+    constexpr bool MASKED = decltype(masked_tag)::value;
+#pragma unroll
+    for (int key0 = 0; key0 < C::KT; key0 += 32) {
+      if (MASKED && kt + key0 >= Nk) break;
+      f32x16 s[2] = {zero16(), zero16()};
+#pragma unroll
+      for (int si = 0; si < C::KS; ++si) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ks + (key0 + r) * C::KROW + 16 * si + 8 * h);
+        s[0] = M::mma(af, qf[0][si], s[0]);
+        s[1] = M::mma(af, qf[1][si], s[1]);
+      }
+      float mx[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        if constexpr (MASKED) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (kt + key0 + acc_row(i, h) >= Nk) s[st][i] = kNegInf;
+        }
+        float v = s[st][0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) v = fmaxf(v, s[st][i]);
+        mx[st] = fmaxf(v, xhalf(v)) * cs;
+      }
+      if (__any(mx[0] > m[0] + kRescaleThr || mx[1] > m[1] + kRescaleThr)) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const float mn = fmaxf(m[st], mx[st]);
+          const float alpha = fast_exp2(m[st] - mn);
+          m[st] = mn;
+#pragma unroll
+          for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[st][t][i] *= alpha;
+        }
+      }
+      bf16x8 pf[2][2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const float nm = -m[st];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[st][i] = fast_exp2(__builtin_fmaf(s[st][i], cs, nm));
+        pf[st][0] = M::p_frag(s[st], 0);
+        pf[st][1] = M::p_frag(s[st], 1);
+      }
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t) {
+          const bf16x8 vf = vt_frag_lds<C::VROW>(Vs, key0, sp, t);
+          o[0][t] = M::mma(vf, pf[0][sp], o[0][t]);
+          o[1][t] = M::mma(vf, pf[1][sp], o[1][t]);
+        }
+    }
+  };
+
+  load_tile(0);
+  int kt = 0;
+  for (; kt + C::KT <= Nk; kt += C::KT) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (kt + C::KT < Nk) load_tile(kt + C::KT);
+    compute_tile(kt, std::false_type{});
+  }
+  if (kt < Nk) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    compute_tile(kt, std::true_type{});
+  }
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const float mine = o[st][C::ONE_T][C::ONE_I];
+    const float other = xhalf(mine);
+    const float lrow = (h == C::ONE_H) ? mine : other;
+    if (qv[st]) {
+      const float inv = 1.f / lrow;
+      T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr[st] * a.o_sf + pos[st] * a.o_sn + head * D;
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dc = 32 * t + 8 * g + 4 * h;
+          if (dc < D) {
+            bf16x4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[st][t][4 * g + j] * inv);
+            *reinterpret_cast<bf16x4*>(orow + dc) = v;
+          }
+        }
+    }
+  }
+}
+
+static int k1_variant() {  // VP2P_K1_VARIANT=0 forces the one-set kernel (A/B experiments)
+  const char* e = getenv("VP2P_K1_VARIANT");
+  return e ? atoi(e) : 2;
+}
+
 template <typename T, int D>
 static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
   using C = FrameCfg<T, D>;
   const int FQ = a->frames * a->tokens_q;
+  if constexpr (C::BF && C::ONES && D <= 64) {
+    if (k1_variant() == 2) {
+      const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
+      if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+      hipLaunchKernelGGL((frame_attn_kernel_x2<D>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);
+      return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+    }
+  }
   const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 127) / 128);
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
   hipLaunchKernelGGL((frame_attn_kernel<T, D>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);
