@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import frame_parallel, ops
 from .controllers import LayerCall
 
 
@@ -84,10 +84,16 @@ class FrameAttention(CrossAttention):
         f = video_length
         B = x.shape[0] // f
         q = F.linear(x, self.to_q.weight, self.to_q.bias)
-        x0 = x.view(B, f, *x.shape[1:])[:, 0]
-        kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
-                      None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
         C = q.shape[-1]
+        shard = frame_parallel.active()
+        if shard is None or shard.rank == 0:   # frame 0 is local (rank 0 owns the first frames)
+            x0 = x.view(B, f, *x.shape[1:])[:, 0]
+            kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
+                          None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
+        else:
+            kv = torch.empty(B, x.shape[1], 2 * C, device=x.device, dtype=q.dtype)
+        if shard is not None:
+            kv = shard.broadcast_(kv.contiguous())
         out = ops.frame_attention(q, kv[..., :C], kv[..., C:], f, self.heads, scale=self.scale)
         return self.to_out[1](self.to_out[0](out))
 
@@ -148,11 +154,16 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
     if module.to_q.bias is not None:
         bias = torch.cat([module.to_q.bias, module.to_k.bias, module.to_v.bias])
     qkv = F.linear(x, w, bias)
+    shard = frame_parallel.active() if temporal_layout == "bf" else None
+    if shard is not None:
+        # frames are sharded: regroup to all frames x this rank's token slice (one all-to-all)
+        B = x.shape[0] // video_length
+        qkv = shard.to_tokens(qkv, B)
     q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
     if temporal_layout == "bf":
-        f = video_length
-        B = x.shape[0] // f
-        N = x.shape[1]
+        f = video_length * (shard.world if shard is not None else 1)
+        B = qkv.shape[0] // f
+        N = qkv.shape[1]
     else:  # the reference's '(b d) f c' tensor
         f = x.shape[1]
         P0 = getattr(controller, "batch_size", 0) or 0
@@ -176,6 +187,8 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
         out = _pv_temporal(module, attn, v, B, f, N, temporal_layout == "bf")
     elif controller is not None:
         controller.fused_end(False, place, call, probs)
+    if shard is not None:
+        out = shard.to_frames(out, B)
     return to_out(out)
 
 

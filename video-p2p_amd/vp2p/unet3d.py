@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import frame_parallel
 from .attention import CrossAttention, FrameAttention
 
 
@@ -40,7 +41,13 @@ def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bo
     G = norm.num_groups
     xv = x.permute(0, 2, 3, 1).reshape(B, frames * H * W, G, C // G)
     xf = xv.float()
-    var, mean = torch.var_mean(xf, dim=(1, 3), keepdim=True, unbiased=False)
+    shard = frame_parallel.active()
+    if shard is not None and frames > 1:
+        # statistics span every rank's frames: one all-reduce of (sum x, sum x^2) per norm
+        mean, var = shard.group_norm_stats(xf, frames * H * W * (C // G))
+        mean, var = mean[:, None, :, None], var[:, None, :, None]
+    else:
+        var, mean = torch.var_mean(xf, dim=(1, 3), keepdim=True, unbiased=False)
     y = (xf - mean) * torch.rsqrt(var + norm.eps)
     y = y.reshape(Bf, H, W, C)
     if norm.affine:
