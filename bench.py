@@ -87,11 +87,29 @@ class K1Timer:
         flops = 4.0 * Bf * N * N * C           # QK^T + PV, frame-0 K/V: 4 * B*f * HW^2 * C
         avg_s = sum(ms) / len(ms) / 1e3
         achieved = flops / avg_s / 1e12
+        esz = 2 if peak == PEAK_BF16_TFLOPS else 4
+        alg_bytes = esz * (2 * Bf * N * C + 2 * (Bf // frames) * N * C)   # Q in + O out + frame-0 K, V
+        traffic, src = _pmc_traffic()
         return {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": src, "algorithmic_bytes": alg_bytes,
                 "kernel": "vp2p::frame_attn_kernel_x2<40> (res-64 FrameAttention, bf16)",
                 "launches": len(ms), "avg_ms": round(sum(ms) / len(ms), 4),
                 "flops_per_launch": flops}
+
+
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "k1_pmc_traffic.json")
+
+
+def _pmc_traffic():
+    """HBM bytes per K1 launch from the committed rocprofv3 --pmc passes (FETCH_SIZE x2 per the gfx950
+    correction, + WRITE_SIZE; tools/pmc_traffic.py) on the same kernel and shape, or None."""
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            d = json.load(fh)
+        return d["bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT) + " (" + d["how"] + ")"
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def cpu_baseline(frames, ddim_steps, threads):
