@@ -146,6 +146,59 @@ typedef struct vp2p_step_args {
 
 int vp2p_step_fused(const vp2p_step_args* args, void* stream);
 
+/* ================================================================================================
+ * Non-attention UNet path.  Activations are channels-last and contiguous:
+ * element (row, c) of a (rows, channels) matrix, row = (sample, h, w) flattened.
+ * ============================================================================================== */
+
+/* ---- K7: 5-D GroupNorm (+ per-sample channel add, + SiLU) ---------------------------------------
+ * Replaces nn.GroupNorm on the (b, c, f, h, w) tensor (statistics over c/G x f x h x w):
+ * tuneavideo/models/resnet.py:142,158 (+ the h + temb add at :149-156 and nonlinearity :143,159),
+ * unet.py:206 (conv_norm_out + SiLU) and Transformer3DModel.norm (attention.py:110, frames = 1).
+ * Two kernels: _stats writes per-chunk (count, mean, M2) partials; _apply merges partials (Chan)
+ * and normalises.  A frame-sharded caller gathers the partials of every rank between the two. */
+typedef struct vp2p_group_norm_args {
+  const void* x;            /* (batch*frames*rows, channels), dtype */
+  const void* add;          /* optional (batch*frames, channels), dtype: added to x before the norm */
+  void* y;                  /* like x; may alias x */
+  const void* weight;       /* (channels) dtype, or NULL (affine off) */
+  const void* bias;         /* (channels) dtype, or NULL */
+  float* partials;          /* (batch, parts, groups, 3) fp32, parts = vp2p_group_norm_parts() */
+  int32_t batch;            /* statistics groups: samples = batch * frames */
+  int32_t frames;           /* samples sharing one set of statistics */
+  int32_t rows;             /* h*w rows per sample */
+  int32_t channels, groups; /* channels % 8 == 0 and <= 4096, channels % groups == 0, groups <= 64 */
+  float eps;
+  int32_t silu;             /* apply x * sigmoid(x) after the affine */
+  int32_t dtype;
+} vp2p_group_norm_args;
+
+int32_t vp2p_group_norm_parts(const vp2p_group_norm_args* args);   /* <0: unsupported shape */
+int vp2p_group_norm_stats(const vp2p_group_norm_args* args, void* stream);
+/* nsets partial arrays laid out back to back, each (batch, parts, groups, 3) */
+int vp2p_group_norm_apply(const vp2p_group_norm_args* args, const float* partials, int32_t nsets,
+                          void* stream);
+int vp2p_group_norm_fwd(const vp2p_group_norm_args* args, void* stream);   /* stats + apply */
+
+/* ---- K8: LayerNorm over the channel axis --------------------------------------------------------
+ * nn.LayerNorm of BasicTransformerBlock.norm1/norm2/norm3/norm_temp (attention.py:200-216). */
+typedef struct vp2p_layer_norm_args {
+  const void* x; void* y;   /* (rows, channels), dtype; y may alias x */
+  const void* weight; const void* bias;   /* (channels) dtype or NULL */
+  int64_t rows;
+  int32_t channels;         /* channels % 8 == 0, <= 2048 */
+  float eps;
+  int32_t dtype;
+} vp2p_layer_norm_args;
+
+int vp2p_layer_norm_fwd(const vp2p_layer_norm_args* args, void* stream);
+
+/* ---- K9: GEGLU gate ------------------------------------------------------------------------------
+ * diffusers 0.11.1 GEGLU.forward after its projection: y = a * gelu(g), (a, g) = proj(x).chunk(2)
+ * (FeedForward of attention.py:190, 259).  x: (rows, 2*inner), y: (rows, inner); exact erf GELU,
+ * rounded like torch's eager ops (gelu result to dtype, then the product). */
+int vp2p_geglu_fwd(const void* x, void* y, int64_t rows, int32_t inner, int32_t dtype, void* stream);
+
 /* ---- introspection ---------------------------------------------------------------------------- */
 int vp2p_abi_version(void);
 /* Head dims with compiled kernel instances, written to out[0..n); returns the count. */

@@ -14,7 +14,7 @@ LIB = os.path.join(ROOT, "video-p2p_amd", "lib", "libvp2p_hip.so")
 
 def _declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t)\s+(vp2p_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t)\s+(vp2p_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_the_exports():
@@ -42,12 +42,20 @@ def test_library_loads_and_reports_abi():
     assert lib.vp2p_cross_kv_workspace_bytes(4, 77, 8, 41, 1) == -3
     assert lib.vp2p_frame_attn_fwd(None, None) == -1
     assert lib.vp2p_temporal_attn_p2p_fwd(None, None) == -1
+    gn = _lib.GroupNormArgs(x=1, y=1, batch=4, frames=8, rows=4096, channels=320, groups=32, eps=1e-5, dtype=1)
+    assert lib.vp2p_group_norm_parts(ctypes.byref(gn)) > 0
+    gn.channels = 324
+    assert lib.vp2p_group_norm_parts(ctypes.byref(gn)) == -4
+    assert lib.vp2p_group_norm_stats(ctypes.byref(gn), None) == -4
+    assert lib.vp2p_layer_norm_fwd(None, None) == -1
+    assert lib.vp2p_geglu_fwd(None, None, 1, 8, 1, None) == -1
 
 
 def test_struct_layout_matches_header(tmp_path):
     from vp2p import _lib
     structs = {"vp2p_frame_attn_args": _lib.FrameAttnArgs, "vp2p_cross_attn_args": _lib.CrossAttnArgs,
-               "vp2p_temporal_attn_args": _lib.TemporalAttnArgs, "vp2p_step_args": _lib.StepArgs}
+               "vp2p_temporal_attn_args": _lib.TemporalAttnArgs, "vp2p_step_args": _lib.StepArgs,
+               "vp2p_group_norm_args": _lib.GroupNormArgs, "vp2p_layer_norm_args": _lib.LayerNormArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

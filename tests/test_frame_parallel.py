@@ -56,6 +56,8 @@ def _cpu_worker(rank, world, port, out_path):
     ok.append(bool((t == 0).all()))
     lat = torch.arange(2 * 3 * f * 2, dtype=torch.float32).reshape(2, 3, f, 2)
     ok.append(torch.equal(sh.gather(sh.local(lat, 2), 2), lat))
+    flat = torch.arange(5, dtype=torch.float32) + 10 * rank
+    ok.append(torch.equal(sh.all_gather_flat(flat), torch.cat([torch.arange(5.0) + 10 * r for r in range(world)])))
     torch.save(ok, out_path + f".{rank}")
     dist.destroy_process_group()
 

@@ -1,0 +1,476 @@
+// K7 (5-D GroupNorm + channel add + SiLU), K8 (LayerNorm), K9 (GEGLU gate): the HBM-bound
+// normalisation / activation work of the UNet3D around the attention kernels.
+//
+// All three read channels-last activations in 16-byte vectors of 8 channels.  A thread owns one
+// 8-channel vector of a row and walks rows, so per-channel parameters (affine, fused scale/shift)
+// stay in registers and every global access is a full, coalesced 16-byte load/store.
+//
+// GroupNorm statistics span (c/G, f, h, w) of one batch element (tuneavideo resnet.py:142,158 runs
+// nn.GroupNorm on the 5-D tensor).  At B=4, f=8, 64x64, C=320 one group is 327,680 elements, so the
+// reduction is split over ~1000 row chunks per launch: gn_stats_kernel writes one
+// (count, mean, M2) partial per (chunk, group) from shifted per-thread sums, gn_apply_kernel merges
+// all partials of its batch element with Chan's formula (parallel over threads, then one merge per
+// group) and applies y = x * a_c + b_c with a_c = rstd_g * w_c, b_c = bias_c - mean_g * a_c.
+// Traffic: x read twice (the second read is usually an Infinity-Cache hit), y written once.
+#include "common.hpp"
+#include "vp2p.h"
+
+namespace vp2p {
+
+template <typename T> struct V8;
+template <> struct V8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float (&v)[8]) {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)r[j];
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float (&v)[8]) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (bf16)v[j];
+    *reinterpret_cast<bf16x8*>(p) = r;
+  }
+  static __device__ __forceinline__ float round(float x) { return (float)(bf16)x; }
+};
+template <> struct V8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
+    const f32x4 a = reinterpret_cast<const f32x4*>(p)[0], b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
+    f32x4 a, b;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { a[j] = v[j]; b[j] = v[4 + j]; }
+    reinterpret_cast<f32x4*>(p)[0] = a;
+    reinterpret_cast<f32x4*>(p)[1] = b;
+  }
+  static __device__ __forceinline__ float round(float x) { return x; }
+};
+
+template <typename T> __device__ __forceinline__ float ld1(const void* p, int i) {
+  return (float)static_cast<const T*>(p)[i];
+}
+
+struct Welford {
+  float n, mean, m2;
+};
+
+__device__ __forceinline__ Welford wmerge(Welford a, Welford b) {
+  const float n = a.n + b.n;
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float d = b.mean - a.mean;
+  const float fb = b.n / n;
+  return {n, a.mean + d * fb, a.m2 + b.m2 + d * d * a.n * fb};
+}
+
+// ------------------------------------------------------------------------------------------------
+// GroupNorm geometry (host and device agree on it): block = nvec * R threads, thread t owns channel
+// vector t % nvec of rows r = t / nvec, r + R, ...; a chunk is `chunk` consecutive rows of one
+// batch element (frames * rows rows in total).
+// ------------------------------------------------------------------------------------------------
+struct GnGeom {
+  int nvec, R, threads, chunk, parts, cg;
+  int64_t L;
+};
+
+static bool gn_geom(const vp2p_group_norm_args* a, GnGeom* g) {
+  if (!a || a->batch <= 0 || a->frames <= 0 || a->rows <= 0 || a->channels <= 0 || a->groups <= 0)
+    return false;
+  if (a->channels % 8 || a->channels % a->groups || a->groups > 64 || a->channels > 4096) return false;
+  g->nvec = a->channels / 8;
+  g->R = a->channels / 8 >= 512 ? 1 : 512 / (a->channels / 8);
+  g->threads = g->nvec * g->R;
+  if (g->threads > 512) return false;
+  g->cg = a->channels / a->groups;
+  g->L = (int64_t)a->frames * a->rows;
+  // ~1024 blocks per launch, at most 16 rows per thread (4 rounds of kUnroll loads in flight)
+  const int64_t all = g->L * a->batch;
+  int64_t rpt = (all + (int64_t)g->R * 1024 - 1) / ((int64_t)g->R * 1024);
+  if (rpt < 1) rpt = 1;
+  if (rpt > 16) rpt = 16;
+  const int64_t chunk = rpt * g->R;
+  g->chunk = (int)chunk;
+  g->parts = (int)((g->L + chunk - 1) / chunk);
+  return true;
+}
+
+constexpr int kUnroll = 4;
+
+// x (+ add of the row's sample) of one 8-channel vector, rounded to T like torch's h + temb
+template <typename T, bool ADD>
+__device__ __forceinline__ void load_row(const vp2p_group_norm_args& a, const T* x, int b, int64_t row, int v,
+                                         float (&val)[8]) {
+  V8<T>::load(x + row * a.channels, val);
+  if (ADD) {
+    float ad[8];
+    V8<T>::load(static_cast<const T*>(a.add) + ((int64_t)b * a.frames + row / a.rows) * a.channels + v * 8, ad);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) val[j] = V8<T>::round(val[j] + ad[j]);
+  }
+}
+
+template <typename T, bool ADD>
+__global__ __launch_bounds__(512) void gn_stats_kernel(const vp2p_group_norm_args a, const GnGeom g) {
+  extern __shared__ float sm[];
+  const int C = a.channels, G = a.groups, R = g.R, nvec = g.nvec, cg = g.cg;
+  float* s_mean = sm;                       // [R][C]
+  float* s_m2 = sm + R * C;                 // [R][C]
+  float* s_cnt = sm + 2 * R * C;            // [R]
+  float* s_w = s_cnt + R;                   // [3][threads] second-stage partials
+  const int b = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
+  const int v = tid % nvec, r = tid / nvec;
+  const int64_t row0 = (int64_t)part * g.chunk;
+  const int64_t row1 = row0 + g.chunk < g.L ? row0 + g.chunk : g.L;
+  const T* x = static_cast<const T*>(a.x) + (int64_t)b * g.L * C + v * 8;
+  float K[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { K[j] = 0.f; s1[j] = 0.f; s2[j] = 0.f; }
+  int n = 0;
+  int64_t row = row0 + r;
+  if (row < row1) load_row<T, ADD>(a, x, b, row, v, K);     // shift: the thread's first value
+  // kUnroll rows in flight per thread: all loads issued before any is consumed
+  for (; row + (kUnroll - 1) * R < row1; row += kUnroll * R) {
+    float val[kUnroll][8];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) load_row<T, ADD>(a, x, b, row + u * R, v, val[u]);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = val[u][j] - K[j];
+        s1[j] += d;
+        s2[j] = fmaf(d, d, s2[j]);
+      }
+    n += kUnroll;
+  }
+  for (; row < row1; row += R) {
+    float val[8];
+    load_row<T, ADD>(a, x, b, row, v, val);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = val[j] - K[j];
+      s1[j] += d;
+      s2[j] = fmaf(d, d, s2[j]);
+    }
+    ++n;
+  }
+  const float fn = (float)n, inv = n ? 1.f / fn : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s_mean[r * C + v * 8 + j] = K[j] + s1[j] * inv;
+    s_m2[r * C + v * 8 + j] = fmaxf(s2[j] - s1[j] * s1[j] * inv, 0.f);
+  }
+  if (v == 0) s_cnt[r] = fn;
+  __syncthreads();
+  // stage 2: tpg threads per group merge the group's R * cg (row-lane, channel) entries
+  const int tpg = g.threads / G;
+  const int gi = tid / tpg, k = tid - gi * tpg;
+  Welford w = {0.f, 0.f, 0.f};
+  if (gi < G) {
+    for (int e = k; e < R * cg; e += tpg) {
+      const int rr = e / cg, c = gi * cg + (e - rr * cg);
+      w = wmerge(w, {s_cnt[rr], s_mean[rr * C + c], s_m2[rr * C + c]});
+    }
+  }
+  s_w[tid] = w.n;
+  s_w[g.threads + tid] = w.mean;
+  s_w[2 * g.threads + tid] = w.m2;
+  __syncthreads();
+  if (tid < G) {
+    Welford t = {0.f, 0.f, 0.f};
+    for (int e = 0; e < tpg; ++e) {
+      const int i = tid * tpg + e;
+      t = wmerge(t, {s_w[i], s_w[g.threads + i], s_w[2 * g.threads + i]});
+    }
+    float* o = a.partials + (((int64_t)b * g.parts + part) * G + tid) * 3;
+    o[0] = t.n;
+    o[1] = t.mean;
+    o[2] = t.m2;
+  }
+}
+
+template <typename T, bool ADD, bool SILU>
+__global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_args a, const GnGeom g,
+                                                        const float* __restrict__ partials, int nsets) {
+  __shared__ float s_w[3 * 512];
+  __shared__ float s_mean[64], s_rstd[64];
+  const int C = a.channels, G = a.groups, R = g.R, nvec = g.nvec, cg = g.cg;
+  const int b = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
+  const int tpg = g.threads / G;
+  const int gi = tid / tpg, k = tid - gi * tpg;
+  Welford w = {0.f, 0.f, 0.f};
+  if (gi < G) {
+    const int total = nsets * g.parts;
+    for (int e = k; e < total; e += tpg) {
+      const int set = e / g.parts, p = e - set * g.parts;
+      const float* q = partials + ((((int64_t)set * a.batch + b) * g.parts + p) * G + gi) * 3;
+      w = wmerge(w, {q[0], q[1], q[2]});
+    }
+  }
+  s_w[tid] = w.n;
+  s_w[512 + tid] = w.mean;
+  s_w[1024 + tid] = w.m2;
+  __syncthreads();
+  if (tid < G) {
+    Welford t = {0.f, 0.f, 0.f};
+    for (int e = 0; e < tpg; ++e) {
+      const int i = tid * tpg + e;
+      t = wmerge(t, {s_w[i], s_w[512 + i], s_w[1024 + i]});
+    }
+    s_mean[tid] = t.mean;
+    s_rstd[tid] = rsqrtf(t.m2 / t.n + a.eps);
+  }
+  __syncthreads();
+  const int v = tid % nvec, r = tid / nvec;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = v * 8 + j, q = c / cg;
+    const float wt = a.weight ? ld1<T>(a.weight, c) : 1.f;
+    const float bs = a.bias ? ld1<T>(a.bias, c) : 0.f;
+    sc[j] = s_rstd[q] * wt;
+    sh[j] = fmaf(-s_mean[q], sc[j], bs);
+  }
+  const int64_t row0 = (int64_t)part * g.chunk;
+  const int64_t row1 = row0 + g.chunk < g.L ? row0 + g.chunk : g.L;
+  const int64_t base = (int64_t)b * g.L * C + v * 8;
+  const T* x = static_cast<const T*>(a.x) + base;
+  T* y = static_cast<T*>(a.y) + base;
+  auto finish = [&](float (&val)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = fmaf(val[j], sc[j], sh[j]);
+      if (SILU) t = t / (1.f + __expf(-t));
+      val[j] = t;
+    }
+  };
+  int64_t row = row0 + r;
+  for (; row + (kUnroll - 1) * R < row1; row += kUnroll * R) {
+    float val[kUnroll][8];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) load_row<T, ADD>(a, x, b, row + u * R, v, val[u]);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      finish(val[u]);
+      V8<T>::store(y + (row + u * R) * C, val[u]);
+    }
+  }
+  for (; row < row1; row += R) {
+    float val[8];
+    load_row<T, ADD>(a, x, b, row, v, val);
+    finish(val);
+    V8<T>::store(y + row * C, val);
+  }
+}
+
+static int gn_check(const vp2p_group_norm_args* a, GnGeom* g) {
+  if (!a || !a->x || !a->y) return VP2P_E_ARG;
+  if (a->dtype != VP2P_F32 && a->dtype != VP2P_BF16) return VP2P_E_DTYPE;
+  if (!gn_geom(a, g)) return VP2P_E_SHAPE;
+  return VP2P_OK;
+}
+
+template <typename T>
+static void gn_stats_launch(const vp2p_group_norm_args& a, const GnGeom& g, hipStream_t s) {
+  const dim3 grid(g.parts, a.batch);
+  const size_t lds = (size_t)(2 * g.R * a.channels + g.R + 3 * g.threads) * sizeof(float);
+  if (a.add)
+    hipLaunchKernelGGL((gn_stats_kernel<T, true>), grid, dim3(g.threads), lds, s, a, g);
+  else
+    hipLaunchKernelGGL((gn_stats_kernel<T, false>), grid, dim3(g.threads), lds, s, a, g);
+}
+
+template <typename T>
+static void gn_apply_launch(const vp2p_group_norm_args& a, const GnGeom& g, const float* parts, int nsets,
+                            hipStream_t s) {
+  const dim3 grid(g.parts, a.batch), block(g.threads);
+  const bool add = a.add != nullptr, silu = a.silu != 0;
+  if (add && silu) hipLaunchKernelGGL((gn_apply_kernel<T, true, true>), grid, block, 0, s, a, g, parts, nsets);
+  else if (add) hipLaunchKernelGGL((gn_apply_kernel<T, true, false>), grid, block, 0, s, a, g, parts, nsets);
+  else if (silu) hipLaunchKernelGGL((gn_apply_kernel<T, false, true>), grid, block, 0, s, a, g, parts, nsets);
+  else hipLaunchKernelGGL((gn_apply_kernel<T, false, false>), grid, block, 0, s, a, g, parts, nsets);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K8 LayerNorm: one wave per row, NV 8-channel vectors per lane held in registers (exact two-pass
+// mean / variance), 4 rows per 256-thread block.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  return x;
+}
+
+template <typename T, int NV, int RPW>
+__global__ __launch_bounds__(256) void ln_kernel(const vp2p_layer_norm_args a) {
+  const int lane = lane_id();
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= a.rows) return;
+  const int C = a.channels, nvec = C / 8;
+  float v[RPW][NV][8];
+  // every load of the wave's RPW rows is issued before the first reduction
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int64_t row = row0 + rr < a.rows ? row0 + rr : a.rows - 1;
+    const T* x = static_cast<const T*>(a.x) + row * C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = lane + 64 * i;
+      if (vi < nvec) {
+        V8<T>::load(x + vi * 8, v[rr][i]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[rr][i][j] = 0.f;
+      }
+    }
+  }
+  float w[NV][8], bs[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = lane + 64 * i;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { w[i][j] = 1.f; bs[i][j] = 0.f; }
+    if (vi < nvec) {
+      if (a.weight) V8<T>::load(static_cast<const T*>(a.weight) + vi * 8, w[i]);
+      if (a.bias) V8<T>::load(static_cast<const T*>(a.bias) + vi * 8, bs[i]);
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int64_t row = row0 + rr;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[rr][i][j];
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (lane + 64 * i < nvec) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[rr][i][j] -= mean;
+          q = fmaf(v[rr][i][j], v[rr][i][j], q);
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)C + a.eps);
+    if (row >= a.rows) continue;
+    T* y = static_cast<T*>(a.y) + row * C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = lane + 64 * i;
+      if (vi < nvec) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[rr][i][j] = v[rr][i][j] * rstd * w[i][j] + bs[i][j];
+        V8<T>::store(y + vi * 8, v[rr][i]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K9 GEGLU gate: y = a * gelu(g) with a = x[:, :inner], g = x[:, inner:]; gelu rounded to the
+// storage type before the product, as torch's eager F.gelu followed by a * (...) does.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void geglu_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t rows,
+                                                    int inner) {
+#pragma clang fp contract(off)
+  const int nv = inner / 8;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * nv) return;
+  const int64_t row = e / nv;
+  const int col = (int)(e - row * nv) * 8;
+  const T* xr = x + row * 2 * inner;
+  float av[8], gv[8];
+  V8<T>::load(xr + col, av);
+  V8<T>::load(xr + inner + col, gv);
+  constexpr float kAlpha = 0.70710678118654752440f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float ge = V8<T>::round(gv[j] * 0.5f * (1.f + erff(gv[j] * kAlpha)));
+    av[j] = av[j] * ge;
+  }
+  V8<T>::store(y + row * inner + col, av);
+}
+
+}  // namespace vp2p
+
+using namespace vp2p;
+
+extern "C" int32_t vp2p_group_norm_parts(const vp2p_group_norm_args* a) {
+  GnGeom g;
+  const int rc = gn_check(a, &g);
+  return rc == VP2P_OK ? g.parts : rc;
+}
+
+extern "C" int vp2p_group_norm_stats(const vp2p_group_norm_args* a, void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!a->partials) return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a->dtype == VP2P_BF16) gn_stats_launch<bf16>(*a, g, s);
+  else gn_stats_launch<float>(*a, g, s);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_apply(const vp2p_group_norm_args* a, const float* partials, int32_t nsets,
+                                     void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!partials || nsets <= 0) return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a->dtype == VP2P_BF16) gn_apply_launch<bf16>(*a, g, partials, nsets, s);
+  else gn_apply_launch<float>(*a, g, partials, nsets, s);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_fwd(const vp2p_group_norm_args* a, void* stream) {
+  int rc = vp2p_group_norm_stats(a, stream);
+  if (rc != VP2P_OK) return rc;
+  return vp2p_group_norm_apply(a, a->partials, 1, stream);
+}
+
+extern "C" int vp2p_layer_norm_fwd(const vp2p_layer_norm_args* a, void* stream) {
+  if (!a || !a->x || !a->y || a->rows < 0) return VP2P_E_ARG;
+  if (a->dtype != VP2P_F32 && a->dtype != VP2P_BF16) return VP2P_E_DTYPE;
+  if (a->channels <= 0 || a->channels % 8 || a->channels > 2048) return VP2P_E_SHAPE;
+  if (a->rows == 0) return VP2P_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nv = (a->channels / 8 + 63) / 64;
+  const int rpw = nv == 1 ? 4 : nv == 2 ? 2 : 1;          // rows per wave: ~4 vector loads in flight per lane
+  const dim3 grid((unsigned)((a->rows + 4 * rpw - 1) / (4 * rpw))), block(256);
+#define VP2P_LN(T)                                                                           \
+  switch (nv) {                                                                              \
+    case 1: hipLaunchKernelGGL((ln_kernel<T, 1, 4>), grid, block, 0, s, *a); break;          \
+    case 2: hipLaunchKernelGGL((ln_kernel<T, 2, 2>), grid, block, 0, s, *a); break;          \
+    case 3: hipLaunchKernelGGL((ln_kernel<T, 3, 1>), grid, block, 0, s, *a); break;          \
+    default: hipLaunchKernelGGL((ln_kernel<T, 4, 1>), grid, block, 0, s, *a); break;         \
+  }
+  if (a->dtype == VP2P_BF16) { VP2P_LN(bf16) } else { VP2P_LN(float) }
+#undef VP2P_LN
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_geglu_fwd(const void* x, void* y, int64_t rows, int32_t inner, int32_t dtype, void* stream) {
+  if (!x || !y || rows < 0 || inner <= 0) return VP2P_E_ARG;
+  if (dtype != VP2P_F32 && dtype != VP2P_BF16) return VP2P_E_DTYPE;
+  if (inner % 8) return VP2P_E_SHAPE;
+  if (rows == 0) return VP2P_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = rows * (inner / 8);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  if (dtype == VP2P_BF16)
+    hipLaunchKernelGGL((geglu_kernel<bf16>), grid, block, 0, s, static_cast<const bf16*>(x), static_cast<bf16*>(y),
+                       rows, inner);
+  else
+    hipLaunchKernelGGL((geglu_kernel<float>), grid, block, 0, s, static_cast<const float*>(x),
+                       static_cast<float*>(y), rows, inner);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}

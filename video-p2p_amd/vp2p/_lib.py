@@ -21,7 +21,21 @@ STATUS = {0: "OK", -1: "VP2P_E_ARG", -2: "VP2P_E_DTYPE", -3: "VP2P_E_HEAD_DIM", 
 
 EXPORTS = ("vp2p_frame_attn_fwd", "vp2p_cross_kv_workspace_bytes", "vp2p_cross_kv_prep",
            "vp2p_cross_attn_p2p_fwd", "vp2p_temporal_attn_p2p_fwd", "vp2p_step_fused",
-           "vp2p_abi_version", "vp2p_supported_head_dims")
+           "vp2p_abi_version", "vp2p_supported_head_dims",
+           "vp2p_group_norm_parts", "vp2p_group_norm_stats", "vp2p_group_norm_apply", "vp2p_group_norm_fwd",
+           "vp2p_layer_norm_fwd", "vp2p_geglu_fwd")
+
+
+class GroupNormArgs(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("add", c_void_p), ("y", c_void_p), ("weight", c_void_p), ("bias", c_void_p),
+                ("partials", c_void_p), ("batch", c_int32), ("frames", c_int32), ("rows", c_int32),
+                ("channels", c_int32), ("groups", c_int32), ("eps", c_float), ("silu", c_int32),
+                ("dtype", c_int32)]
+
+
+class LayerNormArgs(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("weight", c_void_p), ("bias", c_void_p),
+                ("rows", c_int64), ("channels", c_int32), ("eps", c_float), ("dtype", c_int32)]
 
 
 class FrameAttnArgs(ctypes.Structure):
@@ -96,9 +110,17 @@ def load(path: str = None):
     lib.vp2p_temporal_attn_p2p_fwd.argtypes = [POINTER(TemporalAttnArgs), c_void_p]
     lib.vp2p_step_fused.argtypes = [POINTER(StepArgs), c_void_p]
     lib.vp2p_supported_head_dims.argtypes = [POINTER(c_int32), c_int32]
+    gn = POINTER(GroupNormArgs)
+    lib.vp2p_group_norm_parts.argtypes = [gn]
+    lib.vp2p_group_norm_stats.argtypes = [gn, c_void_p]
+    lib.vp2p_group_norm_apply.argtypes = [gn, c_void_p, c_int32, c_void_p]
+    lib.vp2p_group_norm_fwd.argtypes = [gn, c_void_p]
+    lib.vp2p_layer_norm_fwd.argtypes = [POINTER(LayerNormArgs), c_void_p]
+    lib.vp2p_geglu_fwd.argtypes = [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]
     for name in ("vp2p_frame_attn_fwd", "vp2p_cross_kv_prep", "vp2p_cross_attn_p2p_fwd",
                  "vp2p_temporal_attn_p2p_fwd", "vp2p_step_fused", "vp2p_abi_version",
-                 "vp2p_supported_head_dims"):
+                 "vp2p_supported_head_dims", "vp2p_group_norm_parts", "vp2p_group_norm_stats",
+                 "vp2p_group_norm_apply", "vp2p_group_norm_fwd", "vp2p_layer_norm_fwd", "vp2p_geglu_fwd"):
         getattr(lib, name).restype = c_int32
     if lib.vp2p_abi_version() != ABI_VERSION:
         raise Vp2pError(f"{p}: ABI version {lib.vp2p_abi_version()} != {ABI_VERSION}; rebuild")

@@ -119,6 +119,14 @@ class FrameShard:
         dist.all_gather(parts, src, group=self.group)
         return torch.cat(parts, dim=dim).to(x.device)
 
+    def all_gather_flat(self, t: torch.Tensor) -> torch.Tensor:
+        """Every rank's copy of the 1-D tensor ``t`` concatenated in rank order (on t's device):
+        the per-chunk GroupNorm partials (count, mean, M2) of K7, merged by the apply kernel."""
+        src = t.detach().cpu() if (self.staged and t.is_cuda) else t
+        out = torch.empty(self.world * src.numel(), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, src.contiguous(), group=self.group)
+        return out.to(t.device)
+
     def group_norm_stats(self, xv: torch.Tensor, n_local: int):
         """Global (mean, var) per (b, group) of xv (B, L, G, Cg) fp32 summed over dims (1, 3)."""
         s = torch.stack([xv.sum(dim=(1, 3)), (xv * xv).sum(dim=(1, 3))])          # (2, B, G)

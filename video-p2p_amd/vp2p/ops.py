@@ -239,3 +239,87 @@ def step_fused(noise: torch.Tensor, latents: torch.Tensor, consts, guidance: flo
                       _ptr(lb_acc), int(lb_hw[0]), int(lb_hw[1]), float(lb_count), float(lb_th))
     check(_lib.load().vp2p_step_fused(ctypes.byref(a), _stream()), "vp2p_step_fused")
     return out
+
+
+# ----------------------------------------------------------------------------------------------
+# Non-attention UNet path (K7-K9)
+# ----------------------------------------------------------------------------------------------
+def _rows_view(x: torch.Tensor) -> torch.Tensor:
+    """A channels-last activation ((Bf, C, H, W) in channels_last memory, or contiguous (..., C)) as
+    the (rows, C) matrix the kernels read; raises if the memory is not laid out that way."""
+    if x.dim() == 4:
+        if not x.is_contiguous(memory_format=torch.channels_last):
+            raise ValueError("expected a channels_last (Bf, C, H, W) tensor")
+        return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+    if not x.is_contiguous():
+        raise ValueError("expected a contiguous (..., C) tensor")
+    return x.reshape(-1, x.shape[-1])
+
+
+def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
+               eps: float, frames: int, silu: bool = False, add: Optional[torch.Tensor] = None,
+               shard=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GroupNorm of a ``(b f) c h w`` channels-last tensor with statistics over (c/G, f, h, w) of
+    each batch element (tuneavideo resnet.py:142,158; frames=1: per-frame, attention.py:110),
+    optionally on x + add[(b f), c] (the resnet's h + temb, resnet.py:149-156) and followed by SiLU.
+    ``shard``: a FrameShard whose ranks hold the other frames; their partial statistics are
+    gathered between the two kernels."""
+    Bf, C = x.shape[0], x.shape[1]
+    xm = _rows_view(x)
+    dt = _dtype(xm)
+    if Bf % frames:
+        raise ValueError(f"{Bf} samples are not a multiple of {frames} frames")
+    rows = xm.shape[0] // Bf
+    if out is None:
+        out = torch.empty_like(x)
+    ym = _rows_view(out)
+    for t in (weight, bias, add):
+        if t is not None and (t.dtype != x.dtype or not t.is_contiguous() or not t.is_cuda):
+            raise ValueError("weight/bias/add must be contiguous device tensors of the activation dtype")
+    if add is not None and tuple(add.shape) != (Bf, C):
+        raise ValueError(f"add must be (Bf, C) = {(Bf, C)}, got {tuple(add.shape)}")
+    lib = _lib.load()
+    a = _lib.GroupNormArgs(_ptr(xm), _ptr(add), _ptr(ym), _ptr(weight), _ptr(bias), None, Bf // frames, frames,
+                           rows, C, num_groups, float(eps), int(silu), dt)
+    parts = lib.vp2p_group_norm_parts(ctypes.byref(a))
+    if parts < 0:
+        check(parts, "vp2p_group_norm_parts")
+    partials = torch.empty((Bf // frames) * parts * num_groups * 3, device=x.device, dtype=torch.float32)
+    a.partials = partials.data_ptr()
+    s = _stream()
+    check(lib.vp2p_group_norm_stats(ctypes.byref(a), s), "vp2p_group_norm_stats")
+    nsets = 1
+    if shard is not None and shard.world > 1:
+        partials = shard.all_gather_flat(partials)
+        nsets = shard.world
+    check(lib.vp2p_group_norm_apply(ctypes.byref(a), _ptr(partials), nsets, s), "vp2p_group_norm_apply")
+    return out
+
+
+def layer_norm(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor], eps: float,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """nn.LayerNorm over the last (channel) axis (attention.py:200-216)."""
+    if not x.is_contiguous():
+        x = x.contiguous()
+    dt = _dtype(x)
+    C = x.shape[-1]
+    out = torch.empty_like(x) if out is None else out
+    for t in (weight, bias):
+        if t is not None and (t.dtype != x.dtype or not t.is_contiguous()):
+            raise ValueError("weight/bias must be contiguous tensors of the activation dtype")
+    a = _lib.LayerNormArgs(_ptr(x), _ptr(out), _ptr(weight), _ptr(bias), x.numel() // C, C, float(eps), dt)
+    check(_lib.load().vp2p_layer_norm_fwd(ctypes.byref(a), _stream()), "vp2p_layer_norm_fwd")
+    return out
+
+
+def geglu(h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GEGLU gate a * gelu(g) of a (..., 2*inner) projection (diffusers 0.11.1 GEGLU.forward)."""
+    if not h.is_contiguous():
+        h = h.contiguous()
+    dt = _dtype(h)
+    inner = h.shape[-1] // 2
+    if out is None:
+        out = torch.empty(*h.shape[:-1], inner, device=h.device, dtype=h.dtype)
+    check(_lib.load().vp2p_geglu_fwd(_ptr(h), _ptr(out), h.numel() // (2 * inner), inner, dt, _stream()),
+          "vp2p_geglu_fwd")
+    return out

@@ -8,8 +8,11 @@ token view ``(b f) (h w) c`` is what the transformer blocks consume (attention.p
 without a copy.  The 5-D GroupNorms of the reference (statistics over c/G x f x h x w,
 resnet.py:142,158; unet.py:206) are computed on that layout directly.
 
-Only the attention layers run hand-written HIP kernels here; convolutions / GEMMs / norms use
-PyTorch-ROCm (MIOpen / hipBLASLt) -- SURVEY §8(f) rank 1 is the next row to move.
+Hand-written HIP kernels: the attention layers (K1-K3), the 5-D GroupNorm with the resnet's temb
+add and SiLU fused (K7), LayerNorm (K8) and the GEGLU gate (K9).  Convolutions and projection GEMMs
+stay on MIOpen / hipBLASLt.  When autograd must see an op (the null-text optimisation
+differentiates the UNet w.r.t. the unconditional embedding), the norm / gate ops run as PyTorch
+GPU ops so autograd can trace them.
 """
 from __future__ import annotations
 
@@ -21,7 +24,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import frame_parallel
+from . import frame_parallel, ops
 from .attention import CrossAttention, FrameAttention
 
 
@@ -33,16 +36,31 @@ class UNet3DConditionOutput:
         return getattr(self, k)
 
 
-def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bool = False) -> torch.Tensor:
+def _kernel_ok(*ts) -> bool:
+    """The K7-K9 kernels are inference-only: use them unless autograd needs to trace this op."""
+    if not ts[0].is_cuda:
+        return False
+    return not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts))
+
+
+def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bool = False,
+                      add: Optional[torch.Tensor] = None) -> torch.Tensor:
     """GroupNorm whose statistics span ``frames`` consecutive samples of a ``(b f) c h w``
-    channels-last tensor (frames=1: the per-frame GroupNorm of Transformer3DModel.norm)."""
+    channels-last tensor (frames=1: the per-frame GroupNorm of Transformer3DModel.norm), applied
+    to ``x + add[:, :, None, None]`` when ``add`` ((b f), c) is given, then optionally SiLU."""
     Bf, C, H, W = x.shape
+    shard = frame_parallel.active() if frames > 1 else None
+    if _kernel_ok(x, norm.weight, add) and C % 8 == 0 and x.is_contiguous(memory_format=torch.channels_last):
+        return ops.group_norm(x, norm.num_groups, norm.weight if norm.affine else None,
+                              norm.bias if norm.affine else None, norm.eps, frames, silu=silu,
+                              add=None if add is None else add.contiguous(), shard=shard)
+    if add is not None:
+        x = x + add[:, :, None, None].to(x.dtype)
     B = Bf // frames
     G = norm.num_groups
     xv = x.permute(0, 2, 3, 1).reshape(B, frames * H * W, G, C // G)
     xf = xv.float()
-    shard = frame_parallel.active()
-    if shard is not None and frames > 1:
+    if shard is not None:
         # statistics span every rank's frames: one all-reduce of (sum x, sum x^2) per norm
         mean, var = shard.group_norm_stats(xf, frames * H * W * (C // G))
         mean, var = mean[:, None, :, None], var[:, None, :, None]
@@ -55,6 +73,13 @@ def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bo
     if silu:
         y = F.silu(y)
     return y.to(x.dtype).permute(0, 3, 1, 2)
+
+
+def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
+    """nn.LayerNorm over channels on K8 (attention.py:200-216)."""
+    if _kernel_ok(x, norm.weight) and x.shape[-1] % 8 == 0 and norm.elementwise_affine:
+        return ops.layer_norm(x, norm.weight, norm.bias, norm.eps)
+    return norm(x)
 
 
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0) -> torch.Tensor:
@@ -108,9 +133,8 @@ class ResnetBlock3D(nn.Module):
 
     def forward(self, x, temb, frames):
         h = self.conv1(group_norm_frames(x, self.norm1, frames, silu=True))
-        t = self.time_emb_proj(F.silu(temb)).repeat_interleave(frames, 0)
-        h = h + t[:, :, None, None].to(h.dtype)
-        h = self.conv2(self.dropout(group_norm_frames(h, self.norm2, frames, silu=True)))
+        t = self.time_emb_proj(F.silu(temb)).repeat_interleave(frames, 0).to(h.dtype)
+        h = self.conv2(self.dropout(group_norm_frames(h, self.norm2, frames, silu=True, add=t)))
         sc = x if self.conv_shortcut is None else self.conv_shortcut(x)
         out = sc + h
         if self.output_scale_factor != 1.0:
@@ -124,7 +148,10 @@ class GEGLU(nn.Module):
         self.proj = nn.Linear(dim_in, dim_out * 2)
 
     def forward(self, x):
-        a, g = self.proj(x).chunk(2, dim=-1)
+        h = self.proj(x)
+        if _kernel_ok(h) and h.shape[-1] % 16 == 0:
+            return ops.geglu(h)
+        a, g = h.chunk(2, dim=-1)
         return a * F.gelu(g)
 
 
@@ -155,10 +182,10 @@ class BasicTransformerBlock(nn.Module):
         self.norm_temp = nn.LayerNorm(dim)
 
     def forward(self, x, context, frames):
-        x = self.attn1(self.norm1(x), video_length=frames) + x
-        x = self.attn2(self.norm2(x), encoder_hidden_states=context, video_length=frames) + x
-        x = self.ff(self.norm3(x)) + x
-        x = self.attn_temp(self.norm_temp(x), video_length=frames, temporal_layout="bf") + x
+        x = self.attn1(layer_norm(self.norm1, x), video_length=frames) + x
+        x = self.attn2(layer_norm(self.norm2, x), encoder_hidden_states=context, video_length=frames) + x
+        x = self.ff(layer_norm(self.norm3, x)) + x
+        x = self.attn_temp(layer_norm(self.norm_temp, x), video_length=frames, temporal_layout="bf") + x
         return x
 
 
