@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 1
+#define VP2P_ABI_VERSION 2
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -61,9 +61,33 @@ typedef struct vp2p_frame_attn_args {
   int32_t batch, frames, tokens_q, tokens_kv, heads, head_dim;
   float scale;              /* softmax scale (head_dim ** -0.5 in the reference) */
   int32_t dtype;            /* vp2p_dtype of q/k/v/o */
+  float* lse;               /* optional (batch, heads, frames*tokens_q) fp32: log2 of each query row's
+                             * sum_k exp2(score*scale*log2(e)), for the backward; NULL = off */
 } vp2p_frame_attn_args;
 
 int vp2p_frame_attn_fwd(const vp2p_frame_attn_args* args, void* stream);
+
+/* ---- K1b: backward of the shared-K/V attention above (dQ, dK, dV) --------------------------------
+ * Gradient of out = softmax(scale * Q K^T) V where every frame of batch element b attends to the
+ * same keys/values K_b, V_b: FrameAttention (attention.py:282-322) and -- with tokens_kv = 77 --
+ * the plain (uncontrolled) hooked cross-attention (ptp_utils.py:206-220 under the DummyController
+ * of :225-234) that the null-text optimisation differentiates (run_videop2p.py:580-612,
+ * loss.backward() at :601).  P is recomputed from the forward's lse; dK/dV sum over all
+ * frames*tokens_q queries of b.  q, o, dout, dq share the query strides; k, v, dk, dv the key strides. */
+typedef struct vp2p_frame_attn_bwd_args {
+  const void* q; const void* k; const void* v; const void* o; const void* dout;
+  const float* lse;         /* written by vp2p_frame_attn_fwd */
+  void* dq; void* dk; void* dv;
+  void* workspace;          /* vp2p_frame_attn_bwd_workspace_bytes() bytes, 16-byte aligned */
+  int64_t q_sb, q_sf, q_sn; /* (batch, frames, tokens_q) element strides of q, o, dout, dq */
+  int64_t kv_sb, kv_sn;     /* (batch, tokens_kv) element strides of k, v, dk, dv */
+  int32_t batch, frames, tokens_q, tokens_kv, heads, head_dim;
+  float scale;
+  int32_t dtype;
+} vp2p_frame_attn_bwd_args;
+
+int64_t vp2p_frame_attn_bwd_workspace_bytes(const vp2p_frame_attn_bwd_args* args);
+int vp2p_frame_attn_bwd(const vp2p_frame_attn_bwd_args* args, void* stream);
 
 /* ---- K2: hooked cross-attention (<= 128 context tokens) + fused P2P edit --------------------- */
 typedef struct vp2p_cross_attn_args {
@@ -124,6 +148,27 @@ typedef struct vp2p_temporal_attn_args {
 
 int vp2p_temporal_attn_p2p_fwd(const vp2p_temporal_attn_args* args, void* stream);
 
+/* ---- K3b: backward of the plain hooked temporal attention (no self-replace) --------------------
+ * attn_temp under the DummyController (attention.py:262-268 -> ptp_utils.py:206-220, 225-234),
+ * differentiated by the null-text optimisation (run_videop2p.py:601).  All tensors are
+ * (batch, frames, tokens, C) strided views; dq/dk/dv may be views of one (.., 3C) buffer. */
+typedef struct vp2p_temporal_attn_bwd_args {
+  const void* q; const void* k; const void* v; const void* dout;
+  void* dq; void* dk; void* dv;
+  int64_t q_sb, q_sf, q_sn;
+  int64_t k_sb, k_sf, k_sn;
+  int64_t v_sb, v_sf, v_sn;
+  int64_t do_sb, do_sf, do_sn;
+  int64_t dq_sb, dq_sf, dq_sn;
+  int64_t dk_sb, dk_sf, dk_sn;
+  int64_t dv_sb, dv_sf, dv_sn;
+  int32_t batch, frames, tokens, heads, head_dim;   /* frames <= 32, head_dim % 8 == 0 */
+  float scale;
+  int32_t dtype;
+} vp2p_temporal_attn_bwd_args;
+
+int vp2p_temporal_attn_bwd(const vp2p_temporal_attn_bwd_args* args, void* stream);
+
 /* ---- K5+K6: classifier-free guidance + DDIM update + LocalBlend, one launch --------------------
  *   e_p   = cfg ? u_p + g*(t_p - u_p) : n_p        (fast: e_0 = t_0)
  *   x'_p  = c4 * ((x_p - c1*e_p) / c2) + c3*e_p    (each op rounded separately, as torch does)
@@ -145,6 +190,25 @@ typedef struct vp2p_step_args {
 } vp2p_step_args;
 
 int vp2p_step_fused(const vp2p_step_args* args, void* stream);
+
+/* ---- K6b: null-text inner loss + gradient ---------------------------------------------------------
+ * NullInversion.null_optimization (run_videop2p.py:594-599): e = u + g*(c - u),
+ * rec = prev_step(e) = c4*((x - c1*e)/c2) + c3*e, loss = mean((rec - x_prev)^2); writes loss[0] and
+ * grad_uncond = dloss/du (what loss.backward() feeds the UNet).  partials: workspace of
+ * vp2p_nulltext_loss_partials() floats. */
+typedef struct vp2p_nulltext_loss_args {
+  const void* noise_uncond; const void* noise_cond;   /* (n) contiguous, noise_dtype */
+  int32_t noise_dtype;
+  const float* latents; const float* latents_prev;    /* (n) fp32 */
+  void* grad_uncond;                                  /* (n) noise_dtype */
+  float* partials;
+  float* loss;
+  int64_t n;
+  float guidance, c1, c2, c3, c4;
+} vp2p_nulltext_loss_args;
+
+int vp2p_nulltext_loss(const vp2p_nulltext_loss_args* args, void* stream);
+int32_t vp2p_nulltext_loss_partials(void);
 
 /* ================================================================================================
  * Non-attention UNet path.  Activations are channels-last and contiguous:
@@ -198,6 +262,21 @@ int vp2p_layer_norm_fwd(const vp2p_layer_norm_args* args, void* stream);
  * (FeedForward of attention.py:190, 259).  x: (rows, 2*inner), y: (rows, inner); exact erf GELU,
  * rounded like torch's eager ops (gelu result to dtype, then the product). */
 int vp2p_geglu_fwd(const void* x, void* y, int64_t rows, int32_t inner, int32_t dtype, void* stream);
+
+/* ---- K7b-K9b: input gradients of K7-K9 (weights frozen: run_videop2p.py:580-612 optimises only
+ * the unconditional embedding).  GroupNorm: _reduce writes (batch, parts, groups, 2) fp32 partial
+ * sums (sum g, sum g*xhat) from the forward partials; _apply merges bsets such arrays (a
+ * frame-sharded caller gathers them between the two) and writes dx.  `add` / `silu` as in the
+ * forward (d(add) is not produced). */
+int vp2p_group_norm_bwd_reduce(const vp2p_group_norm_args* args, const float* partials, int32_t nsets,
+                               const void* dy, float* bwd_partials, void* stream);
+int vp2p_group_norm_bwd_apply(const vp2p_group_norm_args* args, const float* partials, int32_t nsets,
+                              const void* dy, const float* bwd_partials, int32_t bsets, void* dx,
+                              void* stream);
+int vp2p_layer_norm_bwd(const vp2p_layer_norm_args* args, const void* dy, void* dx, void* stream);
+/* x: the forward input (rows, 2*inner); dy: (rows, inner); dx: (rows, 2*inner) */
+int vp2p_geglu_bwd(const void* x, const void* dy, void* dx, int64_t rows, int32_t inner, int32_t dtype,
+                   void* stream);
 
 /* ---- introspection ---------------------------------------------------------------------------- */
 int vp2p_abi_version(void);

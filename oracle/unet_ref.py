@@ -76,9 +76,21 @@ def frame_attention(sd, p, x, f):
 
 
 def hooked(sd, p, x, ctx, controller, place):
-    """ptp_utils.py:196-221 (torch CPU fp32, global-max softmax, numpy oracle controller)."""
+    """ptp_utils.py:196-221 (torch CPU fp32, global-max softmax, numpy oracle controller).  With no
+    controller (the DummyController of :225-234) it stays in torch, so autograd can differentiate it."""
     is_cross = ctx is not None
     c = ctx if is_cross else x
+    if controller is None:
+        def heads(t):
+            b, n, dim = t.shape
+            return t.reshape(b, n, HEADS, dim // HEADS).permute(0, 2, 1, 3).reshape(b * HEADS, n, dim // HEADS)
+        q, k, v = heads(_lin(x, sd, p + "to_q.")), heads(_lin(c, sd, p + "to_k.")), heads(_lin(c, sd, p + "to_v."))
+        sim = torch.bmm(q, k.transpose(1, 2)) * (q.shape[-1] ** -0.5)
+        e = torch.exp(sim - sim.max())
+        out = torch.bmm(e / e.sum(-1, keepdim=True), v)
+        bh, n, d = out.shape
+        out = out.reshape(bh // HEADS, HEADS, n, d).permute(0, 2, 1, 3).reshape(bh // HEADS, n, HEADS * d)
+        return _lin(out, sd, p + "to_out.0.")
     q = O.heads_to_batch(_lin(x, sd, p + "to_q.").numpy(), HEADS)
     k = O.heads_to_batch(_lin(c, sd, p + "to_k.").numpy(), HEADS)
     v = O.heads_to_batch(_lin(c, sd, p + "to_v.").numpy(), HEADS)
@@ -155,3 +167,45 @@ def unet_forward(sd: Dict[str, torch.Tensor], sample: torch.Tensor, timestep: in
             x = _conv_frames(x, sd, p + "upsamplers.0.conv.")
     x = F.silu(F.group_norm(x, 32, sd["conv_norm_out.weight"], sd["conv_norm_out.bias"], 1e-5))
     return _conv_frames(x, sd, "conv_out.")
+
+
+def _prev_step(ddim: "O.DDIM", eps: torch.Tensor, t: int, x: torch.Tensor) -> torch.Tensor:
+    """NullInversion.prev_step (run_videop2p.py:445-453) in torch ops (differentiable)."""
+    prev_t = t - ddim.num_train_timesteps // ddim.num_inference_steps
+    a_t = torch.tensor(ddim.alphas_cumprod[t])
+    a_prev = torch.tensor(ddim._ac(prev_t))
+    x0 = (x - (1 - a_t) ** 0.5 * eps) / a_t ** 0.5
+    return a_prev ** 0.5 * x0 + (1 - a_prev) ** 0.5 * eps
+
+
+def null_optimization(sd, latents, uncond: torch.Tensor, cond: torch.Tensor, ddim: "O.DDIM",
+                      num_inner_steps: int = 10, epsilon: float = 1e-5, guidance: float = 7.5):
+    """NullInversion.null_optimization (run_videop2p.py:580-612) on the CPU fp32 UNet with torch
+    autograd and torch's Adam.  latents: the DDIM-inversion list [x_0 .. x_T]; returns
+    (per-step optimised unconditional embeddings, every inner loss, final latent)."""
+    out, losses = [], []
+    latent_cur = latents[-1]
+    ts = [int(t) for t in ddim.timesteps]
+    for i, t in enumerate(ts):
+        uncond = uncond.clone().detach()
+        uncond.requires_grad = True
+        opt = torch.optim.Adam([uncond], lr=1e-2 * (1.0 - i / 100.0))
+        latent_prev = latents[len(latents) - i - 2]
+        with torch.no_grad():
+            noise_cond = unet_forward(sd, latent_cur, t, cond)
+        for _ in range(num_inner_steps):
+            noise_uncond = unet_forward(sd, latent_cur, t, uncond)
+            noise = noise_uncond + guidance * (noise_cond - noise_uncond)
+            loss = F.mse_loss(_prev_step(ddim, noise, t, latent_cur), latent_prev)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+            if losses[-1] < epsilon + i * 2e-5:
+                break
+        out.append(uncond[:1].detach())
+        with torch.no_grad():
+            noise = unet_forward(sd, torch.cat([latent_cur] * 2), t, torch.cat([uncond, cond]))
+            u, c = noise.chunk(2)
+            latent_cur = _prev_step(ddim, u + guidance * (c - u), t, latent_cur)
+    return out, losses, latent_cur

@@ -1,0 +1,253 @@
+"""Backward kernels (K1b, K3b, K6b, K7b-K9b) vs torch autograd of the same math on the CPU in fp32,
+and the null-text optimisation (run_videop2p.py:580-612) vs the CPU oracle (oracle/unet_ref.py).
+
+Tolerances (relative to the reference's max |value|): fp32 1e-4 per kernel (1e-3 where a sum runs
+over >10k products), bf16 3e-2 (inputs rounded to bf16, fp32 accumulation)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DT = {"fp32": (torch.float32, 2e-4), "bf16": (torch.bfloat16, 3e-2)}
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _ref_shared(q, kv, frames, heads, scale):
+    Bf, N, C = q.shape
+    B, Nk = kv.shape[0], kv.shape[1]
+    d = C // heads
+    qh = q.reshape(B, frames * N, heads, d).permute(0, 2, 1, 3)
+    k = kv[..., :C].reshape(B, Nk, heads, d).permute(0, 2, 1, 3)
+    v = kv[..., C:].reshape(B, Nk, heads, d).permute(0, 2, 1, 3)
+    s = (qh @ k.transpose(-1, -2)) * scale
+    o = torch.softmax(s, -1) @ v
+    lse2 = torch.logsumexp(s, -1) / np.log(2.0)
+    return o.permute(0, 2, 1, 3).reshape(Bf, N, C), lse2
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("d", [32, 40, 64, 80, 128, 160])
+@pytest.mark.parametrize("frames,N,Nk", [(2, 64, 77), (3, 50, 130)])
+def test_shared_kv_attention_backward(dt, d, frames, N, Nk):
+    from vp2p import autograd
+    dtype, tol = DT[dt]
+    heads, B = 2, 2
+    C = heads * d
+    g = torch.Generator().manual_seed(d + N)
+    q = (torch.randn(B * frames, N, C, generator=g)).to(dtype)
+    kv = (torch.randn(B, Nk, 2 * C, generator=g)).to(dtype)
+    dout = torch.randn(B * frames, N, C, generator=g).to(dtype)
+    scale = d ** -0.5
+    qr, kvr = q.detach().float().clone().requires_grad_(), kv.detach().float().clone().requires_grad_()
+    ref, lse_ref = _ref_shared(qr, kvr, frames, heads, scale)
+    ref.backward(dout.float())
+    qc, kvc = q.detach().cuda().requires_grad_(), kv.detach().cuda().requires_grad_()
+    out = autograd.SharedKVAttention.apply(qc, kvc, frames, heads, scale)
+    out.backward(dout.cuda())
+    assert _rel(out, ref.detach()) < tol
+    assert _rel(qc.grad, qr.grad) < tol, _rel(qc.grad, qr.grad)
+    assert _rel(kvc.grad[..., :C], kvr.grad[..., :C]) < tol, _rel(kvc.grad[..., :C], kvr.grad[..., :C])
+    assert _rel(kvc.grad[..., C:], kvr.grad[..., C:]) < tol, _rel(kvc.grad[..., C:], kvr.grad[..., C:])
+
+
+def test_frame_attention_lse():
+    from vp2p import ops
+    heads, d, B, f, N, Nk = 2, 40, 1, 2, 96, 200
+    C = heads * d
+    g = torch.Generator().manual_seed(5)
+    q = torch.randn(B * f, N, C, generator=g) * 2
+    kv = torch.randn(B, Nk, 2 * C, generator=g) * 2
+    lse = torch.empty(B, heads, f * N, device="cuda")
+    ops.frame_attention(q.cuda(), kv[..., :C].cuda(), kv[..., C:].cuda(), f, heads, lse=lse)
+    _, ref = _ref_shared(q, kv, f, heads, d ** -0.5)
+    assert float((lse.cpu() - ref).abs().max()) < 1e-4
+
+
+def _ref_temporal(qkv, frames, heads, scale):
+    Bf, N, C3 = qkv.shape
+    C = C3 // 3
+    d = C // heads
+    B = Bf // frames
+    t = qkv.reshape(B, frames, N, 3, heads, d).permute(3, 0, 2, 4, 1, 5)   # (3, B, N, h, f, d)
+    q, k, v = t[0], t[1], t[2]
+    o = torch.softmax((q @ k.transpose(-1, -2)) * scale, -1) @ v             # (B, N, h, f, d)
+    return o.permute(0, 3, 1, 2, 4).reshape(Bf, N, C)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("frames,d", [(2, 40), (8, 64), (5, 80), (24, 40), (8, 160)])
+def test_temporal_attention_backward(dt, frames, d):
+    from vp2p import autograd
+    dtype, tol = DT[dt]
+    heads, B, N = 4, 2, 37
+    C = heads * d
+    g = torch.Generator().manual_seed(frames * d)
+    qkv = torch.randn(B * frames, N, 3 * C, generator=g).to(dtype)
+    dout = torch.randn(B * frames, N, C, generator=g).to(dtype)
+    ref_in = qkv.detach().float().clone().requires_grad_()
+    ref = _ref_temporal(ref_in, frames, heads, d ** -0.5)
+    ref.backward(dout.float())
+    x = qkv.detach().cuda().requires_grad_()
+    out = autograd.TemporalAttention.apply(x, frames, heads, d ** -0.5)
+    out.backward(dout.cuda())
+    assert _rel(out, ref.detach()) < tol
+    assert _rel(x.grad, ref_in.grad) < tol, _rel(x.grad, ref_in.grad)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("C,frames,hw,silu,add", [(64, 2, 8, True, False), (320, 3, 16, True, True),
+                                                 (256, 1, 32, False, False), (640, 4, 8, True, True)])
+def test_group_norm_backward(dt, C, frames, hw, silu, add):
+    from vp2p import autograd
+    dtype, tol = DT[dt]
+    B, G = 2, 32
+    g = torch.Generator().manual_seed(C + hw)
+    x = (torch.randn(B * frames, C, hw, hw, generator=g) * 2 + 0.5).to(dtype)
+    a = (torch.randn(B * frames, C, generator=g)).to(dtype) if add else None
+    w = (torch.rand(C, generator=g) + 0.5).to(dtype)
+    b = (torch.randn(C, generator=g) * 0.1).to(dtype)
+    dy = torch.randn(B * frames, C, hw, hw, generator=g).to(dtype)
+    xr = x.detach().float().clone().requires_grad_()
+    h = xr + (a.float()[:, :, None, None] if add else 0)
+    h5 = h.reshape(B, frames, C, hw, hw).permute(0, 2, 1, 3, 4)
+    y5 = F.group_norm(h5, G, w.float(), b.float(), 1e-5)
+    ref = y5.permute(0, 2, 1, 3, 4).reshape(B * frames, C, hw, hw)
+    if silu:
+        ref = F.silu(ref)
+    ref.backward(dy.float())
+    xc = x.detach().cuda().contiguous(memory_format=torch.channels_last).requires_grad_()
+    out = autograd.GroupNormFn.apply(xc, None if a is None else a.cuda(), w.cuda(), b.cuda(), G, 1e-5, frames, silu)
+    out.backward(dy.cuda().contiguous(memory_format=torch.channels_last))
+    assert _rel(out, ref.detach()) < tol
+    assert _rel(xc.grad, xr.grad) < tol * 5, _rel(xc.grad, xr.grad)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("C", [320, 640, 1280])
+def test_layer_norm_backward(dt, C):
+    from vp2p import autograd
+    dtype, tol = DT[dt]
+    g = torch.Generator().manual_seed(C)
+    x = (torch.randn(3, 50, C, generator=g) * 3 + 1).to(dtype)
+    w = (torch.rand(C, generator=g) + 0.5).to(dtype)
+    b = (torch.randn(C, generator=g) * 0.1).to(dtype)
+    dy = torch.randn(3, 50, C, generator=g).to(dtype)
+    xr = x.detach().float().clone().requires_grad_()
+    ref = F.layer_norm(xr, (C,), w.float(), b.float(), 1e-5)
+    ref.backward(dy.float())
+    xc = x.detach().cuda().requires_grad_()
+    out = autograd.LayerNormFn.apply(xc, w.cuda(), b.cuda(), 1e-5)
+    out.backward(dy.cuda())
+    assert _rel(out, ref.detach()) < tol
+    assert _rel(xc.grad, xr.grad) < tol * 5, _rel(xc.grad, xr.grad)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_geglu_backward(dt):
+    from vp2p import autograd
+    dtype, tol = DT[dt]
+    g = torch.Generator().manual_seed(3)
+    h = (torch.randn(2, 70, 2 * 1280, generator=g) * 2).to(dtype)
+    dy = torch.randn(2, 70, 1280, generator=g).to(dtype)
+    hr = h.detach().float().clone().requires_grad_()
+    a_, g_ = hr.chunk(2, -1)
+    ref = a_ * F.gelu(g_)
+    ref.backward(dy.float())
+    hc = h.detach().cuda().requires_grad_()
+    out = autograd.GEGLUFn.apply(hc)
+    out.backward(dy.cuda())
+    assert _rel(out, ref.detach()) < tol
+    assert _rel(hc.grad, hr.grad) < tol, _rel(hc.grad, hr.grad)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_nulltext_loss_and_grad(dt):
+    from oracle import p2p_oracle as O
+    from oracle import unet_ref
+    from vp2p import autograd
+    from vp2p.scheduler import DDIMScheduler
+    dtype, _ = DT[dt]
+    g = torch.Generator().manual_seed(11)
+    u = torch.randn(1, 4, 3, 16, 16, generator=g).to(dtype)
+    c = torch.randn(1, 4, 3, 16, 16, generator=g).to(dtype)
+    x = torch.randn(1, 4, 3, 16, 16, generator=g)
+    xp = torch.randn(1, 4, 3, 16, 16, generator=g)
+    sch = DDIMScheduler()
+    sch.set_timesteps(50)
+    ddim = O.DDIM()
+    ddim.set_timesteps(50)
+    t = 481
+    ur = u.detach().float().clone().requires_grad_()
+    loss_ref = F.mse_loss(unet_ref._prev_step(ddim, ur + 7.5 * (c.float() - ur), t, x), xp)
+    loss_ref.backward()
+    uc = u.detach().cuda().requires_grad_()
+    loss = autograd.NullTextLoss.apply(uc, c.cuda(), x.cuda(), xp.cuda(), sch.prev_step_constants(t), 7.5)
+    loss.backward()
+    assert abs(loss.item() - loss_ref.item()) <= 1e-5 * loss_ref.item()
+    assert _rel(uc.grad, ur.grad) < (1e-5 if dt == "fp32" else 1e-2)
+
+
+# ---------------------------------------------------------------------------------------------
+# Whole-UNet gradient and the null-text loop vs the CPU oracle (small-channel SD-style config)
+# ---------------------------------------------------------------------------------------------
+CFG = dict(block_out_channels=(256, 256, 512, 512), cross_attention_dim=64, attention_head_dim=8)
+
+
+def _tiny(dtype):
+    import vp2p
+    from vp2p.unet3d import UNet3DConditionModel, init_random_
+    unet = init_random_(UNet3DConditionModel(**CFG), seed=0, std=0.05)
+    sd = {k: v.clone() for k, v in unet.state_dict().items()}
+    unet = unet.to("cuda", dtype).to(memory_format=torch.channels_last)
+    vp2p.register_attention_control(type("M", (), {"unet": unet})(), None)
+    return unet, sd
+
+
+@pytest.mark.parametrize("dt,tol", [("fp32", 2e-3), ("bf16", 8e-2)])
+def test_unet_embedding_gradient_matches_oracle(dt, tol):
+    from oracle import unet_ref
+    dtype = DT[dt][0]
+    unet, sd = _tiny(dtype)
+    unet.requires_grad_(False)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(1, 4, 2, 32, 32, generator=g)
+    emb = torch.randn(1, 77, 64, generator=g)
+    w = torch.randn(1, 4, 2, 32, 32, generator=g)
+    er = emb.clone().requires_grad_()
+    (unet_ref.unet_forward(sd, x, 501, er) * w).sum().backward()
+    ec = emb.detach().cuda().requires_grad_()
+    out = unet(x.cuda().to(dtype), 501, ec).sample
+    (out.float() * w.cuda()).sum().backward()
+    assert _rel(ec.grad, er.grad) < tol, _rel(ec.grad, er.grad)
+
+
+def test_null_optimization_matches_oracle():
+    """Two DDIM steps x up to three Adam iterations, fp32: losses, final latent and the optimised
+    embeddings agree with the oracle's run of the reference algorithm."""
+    from oracle import p2p_oracle as O
+    from oracle import unet_ref
+    from vp2p.pipeline import NullInversion, VideoP2PPipeline
+    unet, sd = _tiny(torch.float32)
+    g = torch.Generator().manual_seed(2)
+    x0 = torch.randn(1, 4, 2, 32, 32, generator=g)
+    ctx = torch.randn(2, 77, 64, generator=g)
+    steps = 2
+    ddim = O.DDIM()
+    ddim.set_timesteps(steps)
+    inv = NullInversion(VideoP2PPipeline(unet), num_ddim_steps=steps)
+    inv.init_prompt("", ctx.cuda())
+    lats = inv.ddim_loop(x0.cuda())
+    unc = inv.null_optimization(lats, 3, 1e-5)
+    lats_cpu = [t.cpu() for t in lats]
+    ref_unc, ref_losses, _ = unet_ref.null_optimization(sd, lats_cpu, ctx[:1], ctx[1:], ddim, num_inner_steps=3)
+    assert len(inv.losses) == len(ref_losses)
+    np.testing.assert_allclose(inv.losses, ref_losses, rtol=2e-3)
+    for a, b in zip(unc, ref_unc):
+        diff = (a.cpu() - b).abs()
+        assert float(diff.mean()) < 1e-3 and float(diff.max()) < 2.5e-2

@@ -242,6 +242,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
   } else {
     lrow = lsum + xhalf(lsum);
   }
+  if (a.lse && qv) a.lse[(int64_t)(b * a.heads + head) * FQ + qi] = m + log2f(lrow);
   if (qv) {
     const float inv = 1.f / lrow;
     T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
@@ -420,6 +421,7 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2(const vp2p_frame_
     const float mine = o[st][C::ONE_T][C::ONE_I];
     const float other = xhalf(mine);
     const float lrow = (h == C::ONE_H) ? mine : other;
+    if (a.lse && qv[st]) a.lse[(int64_t)(b * a.heads + head) * FQ + qi[st]] = m[st] + log2f(lrow);
     if (qv[st]) {
       const float inv = 1.f / lrow;
       T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr[st] * a.o_sf + pos[st] * a.o_sn + head * D;

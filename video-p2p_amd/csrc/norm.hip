@@ -398,6 +398,276 @@ __global__ __launch_bounds__(256) void geglu_kernel(const T* __restrict__ x, T* 
   V8<T>::store(y + row * inner + col, av);
 }
 
+
+// ================================================================================================
+// Backward of K7-K9 (input gradients only: the null-text optimisation differentiates the UNet
+// w.r.t. the unconditional embedding with every weight frozen, run_videop2p.py:580-612).
+// ================================================================================================
+
+// mean / rstd of every group of batch element b from the forward partials (all nsets merged)
+__device__ __forceinline__ void gn_group_stats(const vp2p_group_norm_args& a, const GnGeom& g,
+                                               const float* __restrict__ partials, int nsets, int b, float* s_w,
+                                               float* s_mean, float* s_rstd, float* s_n) {
+  const int G = a.groups, tid = threadIdx.x, tpg = g.threads / G;
+  const int gi = tid / tpg, k = tid - gi * tpg;
+  Welford w = {0.f, 0.f, 0.f};
+  if (gi < G) {
+    const int total = nsets * g.parts;
+    for (int e = k; e < total; e += tpg) {
+      const int set = e / g.parts, p = e - set * g.parts;
+      const float* q = partials + ((((int64_t)set * a.batch + b) * g.parts + p) * G + gi) * 3;
+      w = wmerge(w, {q[0], q[1], q[2]});
+    }
+  }
+  s_w[tid] = w.n;
+  s_w[512 + tid] = w.mean;
+  s_w[1024 + tid] = w.m2;
+  __syncthreads();
+  if (tid < G) {
+    Welford t = {0.f, 0.f, 0.f};
+    for (int e = 0; e < tpg; ++e) {
+      const int i = tid * tpg + e;
+      t = wmerge(t, {s_w[i], s_w[512 + i], s_w[1024 + i]});
+    }
+    s_mean[tid] = t.mean;
+    s_rstd[tid] = rsqrtf(t.m2 / t.n + a.eps);
+    s_n[tid] = t.n;
+  }
+  __syncthreads();
+}
+
+// g = dL/d(normalised x) * weight, through the SiLU when it was fused: a = xhat*w + bias,
+// silu'(a) = s(a) (1 + a (1 - s(a)))
+template <bool SILU>
+__device__ __forceinline__ float gn_grad(float dy, float xhat, float wt, float bs) {
+  if (SILU) {
+    const float av = fmaf(xhat, wt, bs);
+    const float sg = 1.f / (1.f + __expf(-av));
+    dy = dy * sg * (1.f + av * (1.f - sg));
+  }
+  return dy * wt;
+}
+
+// per (chunk, group): sum g and sum g * xhat -> bwd partials (batch, parts, groups, 2)
+template <typename T, bool ADD, bool SILU>
+__global__ __launch_bounds__(512) void gn_bwd_reduce_kernel(const vp2p_group_norm_args a, const GnGeom g,
+                                                            const float* __restrict__ partials, int nsets,
+                                                            const T* __restrict__ dy, float* __restrict__ bpart) {
+  extern __shared__ float sm[];
+  const int C = a.channels, G = a.groups, R = g.R, nvec = g.nvec, cg = g.cg;
+  float* s_w = sm;                      // [3 * 512]
+  float* s_mean = sm + 1536;            // [64]
+  float* s_rstd = s_mean + 64;
+  float* s_n = s_rstd + 64;
+  float* s_a = s_n + 64;                // [R][C]
+  float* s_b = s_a + R * C;             // [R][C]
+  const int b = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
+  gn_group_stats(a, g, partials, nsets, b, s_w, s_mean, s_rstd, s_n);
+  const int v = tid % nvec, r = tid / nvec;
+  float mu[8], rs[8], wt[8], bs[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = v * 8 + j, q = c / cg;
+    mu[j] = s_mean[q];
+    rs[j] = s_rstd[q];
+    wt[j] = a.weight ? ld1<T>(a.weight, c) : 1.f;
+    bs[j] = a.bias ? ld1<T>(a.bias, c) : 0.f;
+    s1[j] = 0.f;
+    s2[j] = 0.f;
+  }
+  const int64_t row0 = (int64_t)part * g.chunk;
+  const int64_t row1 = row0 + g.chunk < g.L ? row0 + g.chunk : g.L;
+  const int64_t base = (int64_t)b * g.L * C + v * 8;
+  const T* x = static_cast<const T*>(a.x) + base;
+  for (int64_t row = row0 + r; row < row1; row += R) {
+    float xv[8], dv[8];
+    load_row<T, ADD>(a, x, b, row, v, xv);
+    V8<T>::load(dy + base + row * C, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (xv[j] - mu[j]) * rs[j];
+      const float gg = gn_grad<SILU>(dv[j], xh, wt[j], bs[j]);
+      s1[j] += gg;
+      s2[j] = fmaf(gg, xh, s2[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s_a[r * C + v * 8 + j] = s1[j];
+    s_b[r * C + v * 8 + j] = s2[j];
+  }
+  __syncthreads();
+  const int tpg = g.threads / G;
+  const int gi = tid / tpg, k = tid - gi * tpg;
+  float t1 = 0.f, t2 = 0.f;
+  if (gi < G) {
+    for (int e = k; e < R * cg; e += tpg) {
+      const int rr = e / cg, c = gi * cg + (e - rr * cg);
+      t1 += s_a[rr * C + c];
+      t2 += s_b[rr * C + c];
+    }
+  }
+  __syncthreads();
+  s_w[tid] = t1;
+  s_w[512 + tid] = t2;
+  __syncthreads();
+  if (tid < G) {
+    float u1 = 0.f, u2 = 0.f;
+    for (int e = 0; e < tpg; ++e) {
+      u1 += s_w[tid * tpg + e];
+      u2 += s_w[512 + tid * tpg + e];
+    }
+    float* o = bpart + (((int64_t)b * g.parts + part) * G + tid) * 2;
+    o[0] = u1;
+    o[1] = u2;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) per group
+template <typename T, bool ADD, bool SILU>
+__global__ __launch_bounds__(512) void gn_bwd_apply_kernel(const vp2p_group_norm_args a, const GnGeom g,
+                                                           const float* __restrict__ partials, int nsets,
+                                                           const T* __restrict__ dy, const float* __restrict__ bpart,
+                                                           int bsets, T* __restrict__ dx) {
+  __shared__ float s_w[3 * 512];
+  __shared__ float s_mean[64], s_rstd[64], s_n[64], s_m1[64], s_m2[64];
+  const int C = a.channels, G = a.groups, R = g.R, nvec = g.nvec, cg = g.cg;
+  const int b = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
+  gn_group_stats(a, g, partials, nsets, b, s_w, s_mean, s_rstd, s_n);
+  if (tid < G) {
+    float u1 = 0.f, u2 = 0.f;
+    for (int set = 0; set < bsets; ++set)
+      for (int p = 0; p < g.parts; ++p) {
+        const float* q = bpart + ((((int64_t)set * a.batch + b) * g.parts + p) * G + tid) * 2;
+        u1 += q[0];
+        u2 += q[1];
+      }
+    s_m1[tid] = u1 / s_n[tid];
+    s_m2[tid] = u2 / s_n[tid];
+  }
+  __syncthreads();
+  const int v = tid % nvec, r = tid / nvec;
+  float mu[8], rs[8], wt[8], bs[8], m1[8], m2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = v * 8 + j, q = c / cg;
+    mu[j] = s_mean[q];
+    rs[j] = s_rstd[q];
+    m1[j] = s_m1[q];
+    m2[j] = s_m2[q];
+    wt[j] = a.weight ? ld1<T>(a.weight, c) : 1.f;
+    bs[j] = a.bias ? ld1<T>(a.bias, c) : 0.f;
+  }
+  const int64_t row0 = (int64_t)part * g.chunk;
+  const int64_t row1 = row0 + g.chunk < g.L ? row0 + g.chunk : g.L;
+  const int64_t base = (int64_t)b * g.L * C + v * 8;
+  const T* x = static_cast<const T*>(a.x) + base;
+  for (int64_t row = row0 + r; row < row1; row += R) {
+    float xv[8], dv[8];
+    load_row<T, ADD>(a, x, b, row, v, xv);
+    V8<T>::load(dy + base + row * C, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (xv[j] - mu[j]) * rs[j];
+      const float gg = gn_grad<SILU>(dv[j], xh, wt[j], bs[j]);
+      xv[j] = rs[j] * (gg - m1[j] - xh * m2[j]);
+    }
+    V8<T>::store(dx + base + row * C, xv);
+  }
+}
+
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const vp2p_layer_norm_args a, const T* __restrict__ dy,
+                                                     T* __restrict__ dx) {
+  const int lane = lane_id();
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int C = a.channels, nvec = C / 8;
+  float xv[NV][8], gv[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = lane + 64 * i;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { xv[i][j] = 0.f; gv[i][j] = 0.f; }
+    if (vi < nvec) {
+      V8<T>::load(static_cast<const T*>(a.x) + row * C + vi * 8, xv[i]);
+      V8<T>::load(dy + row * C + vi * 8, gv[i]);
+      float w[8];
+      if (a.weight) {
+        V8<T>::load(static_cast<const T*>(a.weight) + vi * 8, w);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[i][j] *= w[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += xv[i][j];
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (lane + 64 * i < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xv[i][j] -= mean;
+        q = fmaf(xv[i][j], xv[i][j], q);
+      }
+    }
+  const float rstd = rsqrtf(wave_sum(q) / (float)C + a.eps);
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xv[i][j] *= rstd;
+      s1 += gv[i][j];
+      s2 = fmaf(gv[i][j], xv[i][j], s2);
+    }
+  const float m1 = wave_sum(s1) / (float)C, m2 = wave_sum(s2) / (float)C;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = lane + 64 * i;
+    if (vi < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[i][j] = rstd * (gv[i][j] - m1 - xv[i][j] * m2);
+      V8<T>::store(dx + row * C + vi * 8, xv[i]);
+    }
+  }
+}
+
+// y = a * ge, ge = round(gelu(g)):  da = dy * ge,  dg = round(dy * a) * gelu'(g),
+// gelu'(g) = Phi(g) + g * phi(g)  (torch's autograd of the eager a * F.gelu(g))
+template <typename T>
+__global__ __launch_bounds__(256) void geglu_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                        T* __restrict__ dx, int64_t rows, int inner) {
+#pragma clang fp contract(off)
+  const int nv = inner / 8;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * nv) return;
+  const int64_t row = e / nv;
+  const int col = (int)(e - row * nv) * 8;
+  const T* xr = x + row * 2 * inner;
+  float av[8], gv[8], dv[8];
+  V8<T>::load(xr + col, av);
+  V8<T>::load(xr + inner + col, gv);
+  V8<T>::load(dy + row * inner + col, dv);
+  constexpr float kAlpha = 0.70710678118654752440f;
+  constexpr float kBeta = 0.39894228040143267794f;   // 1/sqrt(2 pi)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float cdf = 0.5f * (1.f + erff(gv[j] * kAlpha));
+    const float ge = V8<T>::round(gv[j] * cdf);
+    const float dge = V8<T>::round(dv[j] * av[j]);
+    const float pdf = kBeta * __expf(-0.5f * gv[j] * gv[j]);
+    av[j] = dv[j] * ge;
+    gv[j] = dge * (cdf + gv[j] * pdf);
+  }
+  T* dr = dx + row * 2 * inner;
+  V8<T>::store(dr + col, av);
+  V8<T>::store(dr + inner + col, gv);
+}
+
 }  // namespace vp2p
 
 using namespace vp2p;
@@ -472,5 +742,94 @@ extern "C" int vp2p_geglu_fwd(const void* x, void* y, int64_t rows, int32_t inne
   else
     hipLaunchKernelGGL((geglu_kernel<float>), grid, block, 0, s, static_cast<const float*>(x),
                        static_cast<float*>(y), rows, inner);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_bwd_reduce(const vp2p_group_norm_args* a, const float* partials, int32_t nsets,
+                                          const void* dy, float* bwd_partials, void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!partials || nsets <= 0 || !dy || !bwd_partials) return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(g.parts, a->batch), block(g.threads);
+  const size_t lds = (size_t)(1536 + 192 + 2 * g.R * a->channels) * sizeof(float);
+  const bool add = a->add != nullptr, silu = a->silu != 0;
+#define VP2P_GNB(T)                                                                                          \
+  {                                                                                                          \
+    const T* d = static_cast<const T*>(dy);                                                                  \
+    if (add && silu) hipLaunchKernelGGL((gn_bwd_reduce_kernel<T, true, true>), grid, block, lds, s, *a, g, partials, nsets, d, bwd_partials); \
+    else if (add) hipLaunchKernelGGL((gn_bwd_reduce_kernel<T, true, false>), grid, block, lds, s, *a, g, partials, nsets, d, bwd_partials); \
+    else if (silu) hipLaunchKernelGGL((gn_bwd_reduce_kernel<T, false, true>), grid, block, lds, s, *a, g, partials, nsets, d, bwd_partials); \
+    else hipLaunchKernelGGL((gn_bwd_reduce_kernel<T, false, false>), grid, block, lds, s, *a, g, partials, nsets, d, bwd_partials); \
+  }
+  if (a->dtype == VP2P_BF16) VP2P_GNB(bf16) else VP2P_GNB(float)
+#undef VP2P_GNB
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_bwd_apply(const vp2p_group_norm_args* a, const float* partials, int32_t nsets,
+                                         const void* dy, const float* bwd_partials, int32_t bsets, void* dx,
+                                         void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!partials || nsets <= 0 || !dy || !bwd_partials || bsets <= 0 || !dx) return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(g.parts, a->batch), block(g.threads);
+  const bool add = a->add != nullptr, silu = a->silu != 0;
+#define VP2P_GNA(T)                                                                                          \
+  {                                                                                                          \
+    const T* d = static_cast<const T*>(dy);                                                                  \
+    T* o = static_cast<T*>(dx);                                                                              \
+    if (add && silu) hipLaunchKernelGGL((gn_bwd_apply_kernel<T, true, true>), grid, block, 0, s, *a, g, partials, nsets, d, bwd_partials, bsets, o); \
+    else if (add) hipLaunchKernelGGL((gn_bwd_apply_kernel<T, true, false>), grid, block, 0, s, *a, g, partials, nsets, d, bwd_partials, bsets, o); \
+    else if (silu) hipLaunchKernelGGL((gn_bwd_apply_kernel<T, false, true>), grid, block, 0, s, *a, g, partials, nsets, d, bwd_partials, bsets, o); \
+    else hipLaunchKernelGGL((gn_bwd_apply_kernel<T, false, false>), grid, block, 0, s, *a, g, partials, nsets, d, bwd_partials, bsets, o); \
+  }
+  if (a->dtype == VP2P_BF16) VP2P_GNA(bf16) else VP2P_GNA(float)
+#undef VP2P_GNA
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_layer_norm_bwd(const vp2p_layer_norm_args* a, const void* dy, void* dx, void* stream) {
+  if (!a || !a->x || !dy || !dx || a->rows < 0) return VP2P_E_ARG;
+  if (a->dtype != VP2P_F32 && a->dtype != VP2P_BF16) return VP2P_E_DTYPE;
+  if (a->channels <= 0 || a->channels % 8 || a->channels > 2048) return VP2P_E_SHAPE;
+  if (a->rows == 0) return VP2P_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nv = (a->channels / 8 + 63) / 64;
+  const dim3 grid((unsigned)((a->rows + 3) / 4)), block(256);
+#define VP2P_LNB(T)                                                                                      \
+  {                                                                                                      \
+    const T* d = static_cast<const T*>(dy);                                                              \
+    T* o = static_cast<T*>(dx);                                                                          \
+    switch (nv) {                                                                                        \
+      case 1: hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, block, 0, s, *a, d, o); break;             \
+      case 2: hipLaunchKernelGGL((ln_bwd_kernel<T, 2>), grid, block, 0, s, *a, d, o); break;             \
+      case 3: hipLaunchKernelGGL((ln_bwd_kernel<T, 3>), grid, block, 0, s, *a, d, o); break;             \
+      default: hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, block, 0, s, *a, d, o); break;            \
+    }                                                                                                    \
+  }
+  if (a->dtype == VP2P_BF16) VP2P_LNB(bf16) else VP2P_LNB(float)
+#undef VP2P_LNB
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_geglu_bwd(const void* x, const void* dy, void* dx, int64_t rows, int32_t inner, int32_t dtype,
+                              void* stream) {
+  if (!x || !dy || !dx || rows < 0 || inner <= 0) return VP2P_E_ARG;
+  if (dtype != VP2P_F32 && dtype != VP2P_BF16) return VP2P_E_DTYPE;
+  if (inner % 8) return VP2P_E_SHAPE;
+  if (rows == 0) return VP2P_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = rows * (inner / 8);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  if (dtype == VP2P_BF16)
+    hipLaunchKernelGGL((geglu_bwd_kernel<bf16>), grid, block, 0, s, static_cast<const bf16*>(x),
+                       static_cast<const bf16*>(dy), static_cast<bf16*>(dx), rows, inner);
+  else
+    hipLaunchKernelGGL((geglu_bwd_kernel<float>), grid, block, 0, s, static_cast<const float*>(x),
+                       static_cast<const float*>(dy), static_cast<float*>(dx), rows, inner);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }

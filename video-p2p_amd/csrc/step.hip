@@ -90,9 +90,70 @@ __global__ __launch_bounds__(256) void step_kernel(const vp2p_step_args a) {
   }
 }
 
+// Null-text inner loss (run_videop2p.py:594-599) and its gradient w.r.t. the unconditional noise:
+//   e = u + g (c - u),  rec = c4 ((x - c1 e) / c2) + c3 e,  loss = mean((rec - x_prev)^2)
+//   dloss/du = (2 / n) (rec - x_prev) (c3 - c4 c1 / c2) (1 - g)
+// Pass 1 writes the gradient and one partial sum per block; pass 2 sums the partials in a fixed
+// order (deterministic loss, compared against the early-stop epsilon every inner iteration).
+constexpr int kLossBlocks = 1024;
+
+template <typename TN>
+__global__ __launch_bounds__(256) void nulltext_loss_kernel(const vp2p_nulltext_loss_args a) {
+#pragma clang fp contract(off)
+  __shared__ float red[4];
+  const TN* u = static_cast<const TN*>(a.noise_uncond);
+  const TN* c = static_cast<const TN*>(a.noise_cond);
+  TN* gout = static_cast<TN*>(a.grad_uncond);
+  const float de = a.c3 - a.c4 * a.c1 / a.c2;
+  const float gscale = 2.f / (float)a.n * de * (1.f - a.guidance);
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float uu = (float)u[i], cc = (float)c[i];
+    const float e = uu + a.guidance * (cc - uu);
+    const float x0 = (a.latents[i] - a.c1 * e) / a.c2;
+    const float rec = a.c4 * x0 + a.c3 * e;
+    const float d = rec - a.latents_prev[i];
+    acc += d * d;
+    gout[i] = (TN)(d * gscale);
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) a.partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void nulltext_loss_final_kernel(const vp2p_nulltext_loss_args a, int nblocks) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nblocks; i += blockDim.x) acc += a.partials[i];
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) a.loss[0] = ((red[0] + red[1]) + (red[2] + red[3])) / (float)a.n;
+}
+
 }  // namespace vp2p
 
 using namespace vp2p;
+
+extern "C" int vp2p_nulltext_loss(const vp2p_nulltext_loss_args* a, void* stream) {
+  if (!a || !a->noise_uncond || !a->noise_cond || !a->latents || !a->latents_prev || !a->grad_uncond ||
+      !a->partials || !a->loss || a->n <= 0)
+    return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t want = (a->n + 255) / 256;
+  const int blocks = (int)(want < kLossBlocks ? want : kLossBlocks);
+  if (a->noise_dtype == VP2P_BF16)
+    hipLaunchKernelGGL(nulltext_loss_kernel<bf16>, dim3(blocks), dim3(256), 0, s, *a);
+  else if (a->noise_dtype == VP2P_F32)
+    hipLaunchKernelGGL(nulltext_loss_kernel<float>, dim3(blocks), dim3(256), 0, s, *a);
+  else
+    return VP2P_E_DTYPE;
+  hipLaunchKernelGGL(nulltext_loss_final_kernel, dim3(1), dim3(256), 0, s, *a, blocks);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int32_t vp2p_nulltext_loss_partials(void) { return kLossBlocks; }
 
 extern "C" int vp2p_step_fused(const vp2p_step_args* a, void* stream) {
   if (!a || !a->noise || !a->latents || !a->out) return VP2P_E_ARG;

@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 STATUS = {0: "OK", -1: "VP2P_E_ARG", -2: "VP2P_E_DTYPE", -3: "VP2P_E_HEAD_DIM", -4: "VP2P_E_SHAPE",
@@ -23,7 +23,10 @@ EXPORTS = ("vp2p_frame_attn_fwd", "vp2p_cross_kv_workspace_bytes", "vp2p_cross_k
            "vp2p_cross_attn_p2p_fwd", "vp2p_temporal_attn_p2p_fwd", "vp2p_step_fused",
            "vp2p_abi_version", "vp2p_supported_head_dims",
            "vp2p_group_norm_parts", "vp2p_group_norm_stats", "vp2p_group_norm_apply", "vp2p_group_norm_fwd",
-           "vp2p_layer_norm_fwd", "vp2p_geglu_fwd")
+           "vp2p_layer_norm_fwd", "vp2p_geglu_fwd",
+           "vp2p_frame_attn_bwd_workspace_bytes", "vp2p_frame_attn_bwd", "vp2p_temporal_attn_bwd",
+           "vp2p_group_norm_bwd_reduce", "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd",
+           "vp2p_nulltext_loss", "vp2p_nulltext_loss_partials")
 
 
 class GroupNormArgs(ctypes.Structure):
@@ -45,7 +48,24 @@ class FrameAttnArgs(ctypes.Structure):
                 ("v_sb", c_int64), ("v_sn", c_int64),
                 ("o_sb", c_int64), ("o_sf", c_int64), ("o_sn", c_int64),
                 ("batch", c_int32), ("frames", c_int32), ("tokens_q", c_int32), ("tokens_kv", c_int32),
+                ("heads", c_int32), ("head_dim", c_int32), ("scale", c_float), ("dtype", c_int32),
+                ("lse", c_void_p)]
+
+
+class FrameAttnBwdArgs(ctypes.Structure):
+    _fields_ = [("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("dout", c_void_p),
+                ("lse", c_void_p), ("dq", c_void_p), ("dk", c_void_p), ("dv", c_void_p), ("workspace", c_void_p),
+                ("q_sb", c_int64), ("q_sf", c_int64), ("q_sn", c_int64), ("kv_sb", c_int64), ("kv_sn", c_int64),
+                ("batch", c_int32), ("frames", c_int32), ("tokens_q", c_int32), ("tokens_kv", c_int32),
                 ("heads", c_int32), ("head_dim", c_int32), ("scale", c_float), ("dtype", c_int32)]
+
+
+class TemporalAttnBwdArgs(ctypes.Structure):
+    _fields_ = ([("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("dout", c_void_p),
+                 ("dq", c_void_p), ("dk", c_void_p), ("dv", c_void_p)]
+                + [(f"{t}_s{x}", c_int64) for t in ("q", "k", "v", "do", "dq", "dk", "dv") for x in "bfn"]
+                + [("batch", c_int32), ("frames", c_int32), ("tokens", c_int32), ("heads", c_int32),
+                   ("head_dim", c_int32), ("scale", c_float), ("dtype", c_int32)])
 
 
 class CrossAttnArgs(ctypes.Structure):
@@ -78,6 +98,13 @@ class StepArgs(ctypes.Structure):
                 ("c1", c_float), ("c2", c_float), ("c3", c_float), ("c4", c_float),
                 ("lb_acc", c_void_p), ("lb_h", c_int32), ("lb_w", c_int32), ("lb_count", c_float),
                 ("lb_th", c_float)]
+
+
+class NullTextLossArgs(ctypes.Structure):
+    _fields_ = [("noise_uncond", c_void_p), ("noise_cond", c_void_p), ("noise_dtype", c_int32),
+                ("latents", c_void_p), ("latents_prev", c_void_p), ("grad_uncond", c_void_p),
+                ("partials", c_void_p), ("loss", c_void_p), ("n", c_int64),
+                ("guidance", c_float), ("c1", c_float), ("c2", c_float), ("c3", c_float), ("c4", c_float)]
 
 
 class Vp2pError(RuntimeError):
@@ -117,10 +144,24 @@ def load(path: str = None):
     lib.vp2p_group_norm_fwd.argtypes = [gn, c_void_p]
     lib.vp2p_layer_norm_fwd.argtypes = [POINTER(LayerNormArgs), c_void_p]
     lib.vp2p_geglu_fwd.argtypes = [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]
+    lib.vp2p_frame_attn_bwd_workspace_bytes.argtypes = [POINTER(FrameAttnBwdArgs)]
+    lib.vp2p_frame_attn_bwd_workspace_bytes.restype = c_int64
+    lib.vp2p_frame_attn_bwd.argtypes = [POINTER(FrameAttnBwdArgs), c_void_p]
+    lib.vp2p_temporal_attn_bwd.argtypes = [POINTER(TemporalAttnBwdArgs), c_void_p]
+    lib.vp2p_group_norm_bwd_reduce.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]
+    lib.vp2p_group_norm_bwd_apply.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
+                                              c_void_p]
+    lib.vp2p_layer_norm_bwd.argtypes = [POINTER(LayerNormArgs), c_void_p, c_void_p, c_void_p]
+    lib.vp2p_geglu_bwd.argtypes = [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]
+    lib.vp2p_nulltext_loss.argtypes = [POINTER(NullTextLossArgs), c_void_p]
+    lib.vp2p_nulltext_loss_partials.argtypes = []
     for name in ("vp2p_frame_attn_fwd", "vp2p_cross_kv_prep", "vp2p_cross_attn_p2p_fwd",
                  "vp2p_temporal_attn_p2p_fwd", "vp2p_step_fused", "vp2p_abi_version",
                  "vp2p_supported_head_dims", "vp2p_group_norm_parts", "vp2p_group_norm_stats",
-                 "vp2p_group_norm_apply", "vp2p_group_norm_fwd", "vp2p_layer_norm_fwd", "vp2p_geglu_fwd"):
+                 "vp2p_group_norm_apply", "vp2p_group_norm_fwd", "vp2p_layer_norm_fwd", "vp2p_geglu_fwd",
+                 "vp2p_frame_attn_bwd", "vp2p_temporal_attn_bwd", "vp2p_group_norm_bwd_reduce",
+                 "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd", "vp2p_nulltext_loss",
+                 "vp2p_nulltext_loss_partials"):
         getattr(lib, name).restype = c_int32
     if lib.vp2p_abi_version() != ABI_VERSION:
         raise Vp2pError(f"{p}: ABI version {lib.vp2p_abi_version()} != {ABI_VERSION}; rebuild")

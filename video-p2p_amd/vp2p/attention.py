@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import frame_parallel, ops
+from . import autograd, frame_parallel, ops
 from .controllers import LayerCall
 
 
@@ -86,6 +86,14 @@ class FrameAttention(CrossAttention):
         q = F.linear(x, self.to_q.weight, self.to_q.bias)
         C = q.shape[-1]
         shard = frame_parallel.active()
+        if autograd.needs_grad(q, x):
+            if shard is not None and shard.world > 1:
+                raise NotImplementedError("backward through frame-sharded FrameAttention (run null-text clip-parallel)")
+            x0 = x.view(B, f, *x.shape[1:])[:, 0]
+            kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
+                          None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
+            out = autograd.SharedKVAttention.apply(q, kv, f, self.heads, self.scale)
+            return self.to_out[1](self.to_out[0](out))
         if shard is None or shard.rank == 0:   # frame 0 is local (rank 0 owns the first frames)
             x0 = x.view(B, f, *x.shape[1:])[:, 0]
             kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
@@ -119,12 +127,21 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
     to_out = module.to_out[0] if isinstance(module.to_out, nn.ModuleList) else module.to_out
     dev = x.device
 
+    plain = controller is None or isinstance(controller, DummyController)
     if is_cross:
         B, f, P = _batch_frames(x, controller, video_length)
         N = x.shape[1]
         P = P if B == 2 * P else 0
         # the context is repeated per frame (attention.py:95); project it once per batch row
         ctx = context if context.shape[0] == B else context.reshape(B, f, *context.shape[1:])[:, 0]
+        if autograd.needs_grad(x, ctx):
+            # differentiated (null-text optimisation): only the uncontrolled hook is ever traced there
+            if not plain:
+                raise NotImplementedError("backward through a P2P-controlled attention layer")
+            q = F.linear(x, module.to_q.weight, module.to_q.bias)
+            kv = F.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
+                          None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))
+            return to_out(autograd.SharedKVAttention.apply(q, kv, f, h, module.scale))
         q = F.linear(x, module.to_q.weight, module.to_q.bias)
         k = F.linear(ctx, module.to_k.weight, module.to_k.bias).contiguous()
         v = F.linear(ctx, module.to_v.weight, module.to_v.bias).contiguous()
@@ -154,6 +171,13 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
     if module.to_q.bias is not None:
         bias = torch.cat([module.to_q.bias, module.to_k.bias, module.to_v.bias])
     qkv = F.linear(x, w, bias)
+    if autograd.needs_grad(qkv):
+        if not plain or temporal_layout != "bf":
+            raise NotImplementedError("backward through a P2P-controlled or '(b d) f c' temporal attention")
+        sh = frame_parallel.active()
+        if sh is not None and sh.world > 1:
+            raise NotImplementedError("backward through frame-sharded temporal attention (run null-text clip-parallel)")
+        return to_out(autograd.TemporalAttention.apply(qkv, video_length, h, module.scale))
     shard = frame_parallel.active() if temporal_layout == "bf" else None
     if shard is not None:
         # frames are sharded: regroup to all frames x this rank's token slice (one all-to-all)

@@ -1,0 +1,149 @@
+"""Autograd wrappers of the HIP kernels, for the null-text optimisation.
+
+``NullInversion.null_optimization`` (run_videop2p.py:580-612) back-propagates an MSE on the DDIM
+step through the whole UNet to the unconditional text embedding.  Convolutions and projection GEMMs
+differentiate through PyTorch (MIOpen / hipBLASLt); every op this package implements as a HIP kernel
+gets its backward as a HIP kernel too:
+
+* ``SharedKVAttention``  K1 forward (+ row lse) / K1b backward -- FrameAttention (attention.py:282-322)
+  and the plain hooked cross-attention (ptp_utils.py:206-220 under the DummyController)
+* ``TemporalAttention``  K3 forward / K3b backward -- plain hooked attn_temp (attention.py:262-268)
+* ``GroupNormFn``        K7 / K7b,  ``LayerNormFn`` K8 / K8b,  ``GEGLUFn`` K9 / K9b
+
+Only input gradients exist: the reference optimises the embedding alone (its Adam holds
+``[uncond_embeddings]``, run_videop2p.py:589), so weight gradients are never consumed; asking for
+one raises instead of returning a silent zero.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+
+def needs_grad(*ts) -> bool:
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+def _no_weight_grad(ctx, *idx):
+    for i in idx:
+        if ctx.needs_input_grad[i]:
+            raise NotImplementedError("vp2p kernels provide input gradients only (freeze the UNet weights: "
+                                      "the null-text optimisation trains the embedding alone)")
+
+
+class SharedKVAttention(torch.autograd.Function):
+    """softmax(scale q k^T) v with the keys/values of batch element b shared by its `frames` frames.
+    q: (B*f, N, C); kv: (B, Nk, 2C) = [K | V]."""
+
+    @staticmethod
+    def forward(ctx, q, kv, frames: int, heads: int, scale: float):
+        q = q.contiguous()
+        kv = kv.contiguous()
+        C = q.shape[-1]
+        B = q.shape[0] // frames
+        lse = torch.empty(B, heads, frames * q.shape[1], device=q.device, dtype=torch.float32)
+        out = ops.frame_attention(q, kv[..., :C], kv[..., C:], frames, heads, scale=scale, lse=lse)
+        ctx.save_for_backward(q, kv, out, lse)
+        ctx.cfg = (frames, heads, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, kv, out, lse = ctx.saved_tensors
+        frames, heads, scale = ctx.cfg
+        C = q.shape[-1]
+        dout = dout.contiguous()
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        ops.frame_attention_bwd(q, kv[..., :C], kv[..., C:], out, dout, lse, frames, heads, scale,
+                                dq, dkv[..., :C], dkv[..., C:])
+        return dq, dkv, None, None, None
+
+
+class TemporalAttention(torch.autograd.Function):
+    """Plain attention over frames per (b, token, head); qkv: (B*f, N, 3C) = [Q | K | V]."""
+
+    @staticmethod
+    def forward(ctx, qkv, frames: int, heads: int, scale: float):
+        qkv = qkv.contiguous()
+        C = qkv.shape[-1] // 3
+        out = ops.temporal_attention_p2p(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], frames, heads,
+                                         scale=scale)
+        ctx.save_for_backward(qkv)
+        ctx.cfg = (frames, heads, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (qkv,) = ctx.saved_tensors
+        frames, heads, scale = ctx.cfg
+        C = qkv.shape[-1] // 3
+        dqkv = torch.empty_like(qkv)
+        ops.temporal_attention_bwd(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], dout.contiguous(), frames,
+                                   heads, scale, dqkv[..., :C], dqkv[..., C:2 * C], dqkv[..., 2 * C:])
+        return dqkv, None, None, None
+
+
+class GroupNormFn(torch.autograd.Function):
+    """5-D GroupNorm (+ channel add, + SiLU) of a channels-last '(b f) c h w' tensor."""
+
+    @staticmethod
+    def forward(ctx, x, add, weight, bias, groups: int, eps: float, frames: int, silu: bool):
+        out, stats = ops.group_norm(x, groups, weight, bias, eps, frames, silu=silu, add=add, return_stats=True)
+        ctx.save_for_backward(x, add, weight, bias, stats[0])
+        ctx.cfg = (groups, eps, frames, silu, stats[1])
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        _no_weight_grad(ctx, 1, 2, 3)
+        x, add, weight, bias, partials = ctx.saved_tensors
+        groups, eps, frames, silu, nsets = ctx.cfg
+        dx = ops.group_norm_bwd(x, dy, (partials, nsets), groups, weight, bias, eps, frames, silu=silu, add=add)
+        return dx, None, None, None, None, None, None, None
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps: float):
+        x = x.contiguous()
+        ctx.save_for_backward(x, weight)
+        ctx.eps = eps
+        return ops.layer_norm(x, weight, bias, eps)
+
+    @staticmethod
+    def backward(ctx, dy):
+        _no_weight_grad(ctx, 1, 2)
+        x, weight = ctx.saved_tensors
+        return ops.layer_norm_bwd(x, dy, weight, ctx.eps), None, None, None
+
+
+class GEGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h):
+        h = h.contiguous()
+        ctx.save_for_backward(h)
+        return ops.geglu(h)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (h,) = ctx.saved_tensors
+        return ops.geglu_bwd(h, dy)
+
+
+class NullTextLoss(torch.autograd.Function):
+    """loss = mse(prev_step(u + g (c - u), t, x), x_prev) of run_videop2p.py:594-599 on K6b; the
+    gradient w.r.t. the unconditional noise u comes out of the same pass."""
+
+    @staticmethod
+    def forward(ctx, noise_uncond, noise_cond, latents, latents_prev, consts, guidance: float):
+        loss, grad = ops.nulltext_loss(noise_uncond.contiguous(), noise_cond.contiguous(), latents.contiguous(),
+                                       latents_prev.contiguous(), consts, guidance)
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (grad,) = ctx.saved_tensors
+        return grad * dloss.to(grad.dtype), None, None, None, None, None

@@ -55,9 +55,11 @@ def _bd_strides(t: torch.Tensor, tokens: int):
 
 # ----------------------------------------------------------------------------------------------
 def frame_attention(q: torch.Tensor, k0: torch.Tensor, v0: torch.Tensor, frames: int, heads: int,
-                    scale: Optional[float] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
+                    lse: Optional[torch.Tensor] = None) -> torch.Tensor:
     """FrameAttention core (attention.py:282-322).  q: (B*f, N, C); k0, v0: frame-0 keys/values
-    (B, Nk, C) -- or full (B*f, Nk, C) tensors, of which only frame 0 is read."""
+    (B, Nk, C) -- or full (B*f, Nk, C) tensors, of which only frame 0 is read.  ``lse``: optional
+    (B, heads, f*N) fp32 output of each row's log2-sum-exp2 (saved for the backward)."""
     dt = _dtype(q, k0, v0)
     Bf, N, C = q.shape
     B = Bf // frames
@@ -75,9 +77,55 @@ def frame_attention(q: torch.Tensor, k0: torch.Tensor, v0: torch.Tensor, frames:
     a = _lib.FrameAttnArgs(_ptr(q), _ptr(k0), _ptr(v0), _ptr(out), q_sb, q_sf, q_sn,
                            k_sb, k0.stride(1), v_sb, v0.stride(1), o_sb, o_sf, o_sn,
                            B, frames, N, k0.shape[1], heads, d,
-                           float(d ** -0.5 if scale is None else scale), dt)
+                           float(d ** -0.5 if scale is None else scale), dt, _ptr(lse))
+    if lse is not None and (lse.dtype != torch.float32 or not lse.is_contiguous()
+                            or lse.numel() != B * heads * frames * N):
+        raise ValueError("lse must be a contiguous fp32 (B, heads, f*N) tensor")
     check(_lib.load().vp2p_frame_attn_fwd(ctypes.byref(a), _stream()), "vp2p_frame_attn_fwd")
     return out
+
+
+def frame_attention_bwd(q, k, v, o, dout, lse, frames: int, heads: int, scale: float,
+                        dq: torch.Tensor, dk: torch.Tensor, dv: torch.Tensor) -> None:
+    """Backward of ``frame_attention`` (K1b): fills dq (like q) and dk, dv (like k, v).  q, o, dout
+    and dq must share their (b f, n) strides; k, v, dk and dv theirs (e.g. views of one K|V
+    buffer and of its gradient)."""
+    dt = _dtype(q, k, v, o, dout, dq, dk, dv)
+    Bf, N, C = q.shape
+    B = Bf // frames
+    for t in (o, dout, dq):
+        if t.shape != q.shape or t.stride() != q.stride():
+            raise ValueError("q, o, dout, dq must share shape and strides")
+    for t in (v, dk, dv):
+        if t.shape != k.shape or t.stride() != k.stride():
+            raise ValueError("k, v, dk, dv must share shape and strides")
+    if k.shape[0] != B:
+        raise ValueError("k/v must be (B, Nk, C)")
+    q_sb, q_sf, q_sn = _bf_strides(q, frames)
+    a = _lib.FrameAttnBwdArgs(_ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(dout), _ptr(lse), _ptr(dq), _ptr(dk),
+                              _ptr(dv), None, q_sb, q_sf, q_sn, k.stride(0), k.stride(1),
+                              B, frames, N, k.shape[1], heads, C // heads, float(scale), dt)
+    lib = _lib.load()
+    nbytes = lib.vp2p_frame_attn_bwd_workspace_bytes(ctypes.byref(a))
+    if nbytes < 0:
+        check(int(nbytes), "vp2p_frame_attn_bwd_workspace_bytes")
+    ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=q.device)
+    a.workspace = ws.data_ptr()
+    check(lib.vp2p_frame_attn_bwd(ctypes.byref(a), _stream()), "vp2p_frame_attn_bwd")
+
+
+def temporal_attention_bwd(q, k, v, dout, frames: int, heads: int, scale: float, dq, dk, dv) -> None:
+    """Backward of the plain hooked temporal attention (K3b) on '(b f) n c' tensors (B*f, N, C)."""
+    dt = _dtype(q, k, v, dout, dq, dk, dv)
+    Bf, N, C = q.shape
+    st = []
+    for t in (q, k, v, dout, dq, dk, dv):
+        if t.shape != q.shape:
+            raise ValueError("temporal backward: shape mismatch")
+        st += list(_bf_strides(t, frames))
+    a = _lib.TemporalAttnBwdArgs(_ptr(q), _ptr(k), _ptr(v), _ptr(dout), _ptr(dq), _ptr(dk), _ptr(dv), *st,
+                                 Bf // frames, frames, N, heads, C // heads, float(scale), dt)
+    check(_lib.load().vp2p_temporal_attn_bwd(ctypes.byref(a), _stream()), "vp2p_temporal_attn_bwd")
 
 
 # ----------------------------------------------------------------------------------------------
@@ -241,6 +289,29 @@ def step_fused(noise: torch.Tensor, latents: torch.Tensor, consts, guidance: flo
     return out
 
 
+def nulltext_loss(noise_uncond: torch.Tensor, noise_cond: torch.Tensor, latents: torch.Tensor,
+                  latents_prev: torch.Tensor, consts, guidance: float = 7.5):
+    """Null-text inner loss mean((prev_step(u + g (c - u)) - x_prev)^2) and its gradient w.r.t. u
+    (run_videop2p.py:594-599) in one pass.  Returns (loss (0-d fp32 tensor), grad like u)."""
+    for t in (noise_uncond, noise_cond, latents, latents_prev):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("nulltext_loss: contiguous device tensors expected")
+    n = noise_uncond.numel()
+    if noise_cond.dtype != noise_uncond.dtype or any(t.numel() != n for t in (noise_cond, latents, latents_prev)):
+        raise ValueError("nulltext_loss: shape/dtype mismatch")
+    if latents.dtype != torch.float32 or latents_prev.dtype != torch.float32:
+        raise ValueError("nulltext_loss: latents must be fp32")
+    lib = _lib.load()
+    grad = torch.empty_like(noise_uncond)
+    parts = torch.empty(lib.vp2p_nulltext_loss_partials() + 1, device=latents.device, dtype=torch.float32)
+    c1, c2, c3, c4 = (float(c) for c in consts)
+    a = _lib.NullTextLossArgs(_ptr(noise_uncond), _ptr(noise_cond), _DT[noise_uncond.dtype], _ptr(latents),
+                              _ptr(latents_prev), _ptr(grad), _ptr(parts[1:]), _ptr(parts), n, float(guidance),
+                              c1, c2, c3, c4)
+    check(lib.vp2p_nulltext_loss(ctypes.byref(a), _stream()), "vp2p_nulltext_loss")
+    return parts[0], grad
+
+
 # ----------------------------------------------------------------------------------------------
 # Non-attention UNet path (K7-K9)
 # ----------------------------------------------------------------------------------------------
@@ -256,31 +327,37 @@ def _rows_view(x: torch.Tensor) -> torch.Tensor:
     return x.reshape(-1, x.shape[-1])
 
 
-def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
-               eps: float, frames: int, silu: bool = False, add: Optional[torch.Tensor] = None,
-               shard=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """GroupNorm of a ``(b f) c h w`` channels-last tensor with statistics over (c/G, f, h, w) of
-    each batch element (tuneavideo resnet.py:142,158; frames=1: per-frame, attention.py:110),
-    optionally on x + add[(b f), c] (the resnet's h + temb, resnet.py:149-156) and followed by SiLU.
-    ``shard``: a FrameShard whose ranks hold the other frames; their partial statistics are
-    gathered between the two kernels."""
+def _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out):
     Bf, C = x.shape[0], x.shape[1]
     xm = _rows_view(x)
     dt = _dtype(xm)
     if Bf % frames:
         raise ValueError(f"{Bf} samples are not a multiple of {frames} frames")
     rows = xm.shape[0] // Bf
-    if out is None:
-        out = torch.empty_like(x)
-    ym = _rows_view(out)
+    ym = _rows_view(out) if out is not None else None
     for t in (weight, bias, add):
         if t is not None and (t.dtype != x.dtype or not t.is_contiguous() or not t.is_cuda):
             raise ValueError("weight/bias/add must be contiguous device tensors of the activation dtype")
     if add is not None and tuple(add.shape) != (Bf, C):
         raise ValueError(f"add must be (Bf, C) = {(Bf, C)}, got {tuple(add.shape)}")
+    return _lib.GroupNormArgs(_ptr(xm), _ptr(add), _ptr(ym), _ptr(weight), _ptr(bias), None, Bf // frames, frames,
+                              rows, C, num_groups, float(eps), int(silu), dt)
+
+
+def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
+               eps: float, frames: int, silu: bool = False, add: Optional[torch.Tensor] = None,
+               shard=None, out: Optional[torch.Tensor] = None, return_stats: bool = False):
+    """GroupNorm of a ``(b f) c h w`` channels-last tensor with statistics over (c/G, f, h, w) of
+    each batch element (tuneavideo resnet.py:142,158; frames=1: per-frame, attention.py:110),
+    optionally on x + add[(b f), c] (the resnet's h + temb, resnet.py:149-156) and followed by SiLU.
+    ``shard``: a FrameShard whose ranks hold the other frames; their partial statistics are
+    gathered between the two kernels.  ``return_stats``: also return (partials, nsets), the
+    statistics the backward needs."""
+    Bf = x.shape[0]
+    if out is None:
+        out = torch.empty_like(x)
+    a = _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out)
     lib = _lib.load()
-    a = _lib.GroupNormArgs(_ptr(xm), _ptr(add), _ptr(ym), _ptr(weight), _ptr(bias), None, Bf // frames, frames,
-                           rows, C, num_groups, float(eps), int(silu), dt)
     parts = lib.vp2p_group_norm_parts(ctypes.byref(a))
     if parts < 0:
         check(parts, "vp2p_group_norm_parts")
@@ -293,7 +370,32 @@ def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor],
         partials = shard.all_gather_flat(partials)
         nsets = shard.world
     check(lib.vp2p_group_norm_apply(ctypes.byref(a), _ptr(partials), nsets, s), "vp2p_group_norm_apply")
+    if return_stats:
+        return out, (partials, nsets)
     return out
+
+
+def group_norm_bwd(x: torch.Tensor, dy: torch.Tensor, stats, num_groups: int, weight, bias, eps: float,
+                   frames: int, silu: bool = False, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Input gradient of ``group_norm`` (K7b) given the forward's ``stats`` = (partials, nsets);
+    dy and the result are channels-last like x."""
+    partials, nsets = stats
+    if not dy.is_contiguous(memory_format=torch.channels_last):
+        dy = dy.contiguous(memory_format=torch.channels_last)
+    dx = torch.empty_like(x, memory_format=torch.channels_last)
+    a = _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, dx)   # y is not read by the backward
+    lib = _lib.load()
+    parts = lib.vp2p_group_norm_parts(ctypes.byref(a))
+    if parts < 0:
+        check(parts, "vp2p_group_norm_parts")
+    bpart = torch.empty((x.shape[0] // frames) * parts * num_groups * 2, device=x.device, dtype=torch.float32)
+    s = _stream()
+    dym = _rows_view(dy)
+    check(lib.vp2p_group_norm_bwd_reduce(ctypes.byref(a), _ptr(partials), nsets, _ptr(dym), _ptr(bpart), s),
+          "vp2p_group_norm_bwd_reduce")
+    check(lib.vp2p_group_norm_bwd_apply(ctypes.byref(a), _ptr(partials), nsets, _ptr(dym), _ptr(bpart), 1,
+                                        _ptr(_rows_view(dx)), s), "vp2p_group_norm_bwd_apply")
+    return dx
 
 
 def layer_norm(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor], eps: float,
@@ -323,3 +425,27 @@ def geglu(h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     check(_lib.load().vp2p_geglu_fwd(_ptr(h), _ptr(out), h.numel() // (2 * inner), inner, dt, _stream()),
           "vp2p_geglu_fwd")
     return out
+
+
+def layer_norm_bwd(x: torch.Tensor, dy: torch.Tensor, weight: Optional[torch.Tensor], eps: float) -> torch.Tensor:
+    """Input gradient of ``layer_norm`` (K8b)."""
+    x = x.contiguous()
+    dy = dy.contiguous()
+    dt = _dtype(x, dy)
+    C = x.shape[-1]
+    dx = torch.empty_like(x)
+    a = _lib.LayerNormArgs(_ptr(x), None, _ptr(weight), None, x.numel() // C, C, float(eps), dt)
+    check(_lib.load().vp2p_layer_norm_bwd(ctypes.byref(a), _ptr(dy), _ptr(dx), _stream()), "vp2p_layer_norm_bwd")
+    return dx
+
+
+def geglu_bwd(h: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    """Gradient of ``geglu`` w.r.t. its (..., 2*inner) input (K9b)."""
+    h = h.contiguous()
+    dy = dy.contiguous()
+    dt = _dtype(h, dy)
+    inner = h.shape[-1] // 2
+    dh = torch.empty_like(h)
+    check(_lib.load().vp2p_geglu_bwd(_ptr(h), _ptr(dy), _ptr(dh), h.numel() // (2 * inner), inner, dt, _stream()),
+          "vp2p_geglu_bwd")
+    return dh

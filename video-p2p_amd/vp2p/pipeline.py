@@ -7,9 +7,10 @@ controller's step callback (LocalBlend).  With a vp2p controller the CFG + DDIM 
 of every step is ONE kernel (``ops.step_fused``).  VAE decoding is out of scope: the pipeline
 returns latents (``output_type="latent"``).
 
-``NullInversion.ddim_loop`` / ``invert_`` follow run_videop2p.py:557-567 / :626-635 on latents
-(image loading and the VAE encoder are out of scope).  Null-text optimisation (``invert``,
-:580-624) needs attention backward kernels and is not implemented yet.
+``NullInversion.ddim_loop`` / ``invert_`` / ``invert`` follow run_videop2p.py:557-567 / :626-635 /
+:614-624 on latents (image loading and the VAE encoder are out of scope).  ``null_optimization``
+(:580-612) back-propagates through the UNet on the HIP backward kernels (``vp2p.autograd``); its
+loss and dloss/du come from one kernel (K6b).
 """
 from __future__ import annotations
 
@@ -18,6 +19,7 @@ from typing import List, Optional, Union
 import torch
 
 from . import ops
+from .attention import register_attention_control
 from .scheduler import DDIMScheduler
 
 NUM_DDIM_STEPS = 50
@@ -134,8 +136,71 @@ class NullInversion:
     def invert_(self, latent: torch.Tensor, prompt: str, text_embeddings: Optional[torch.Tensor] = None):
         """Fast mode (run_videop2p.py:626-635): DDIM inversion only; returns (latents list, x_T, None)."""
         self.init_prompt(prompt, text_embeddings)
+        register_attention_control(self.model, None)
         lats = self.ddim_loop(latent)
         return lats, lats[-1], None
 
-    def invert(self, *a, **k):
-        raise NotImplementedError("null-text optimisation needs attention backward kernels (SURVEY §8(f) rank 2)")
+    @torch.no_grad()
+    def get_noise_pred(self, latents, t, is_forward: bool = True, context=None):
+        """run_videop2p.py:473-490: CFG over [uncond, cond] (guidance 1 forward, 7.5 backward) + step."""
+        if context is None:
+            context = self.context
+        g = 1.0 if is_forward else GUIDANCE_SCALE
+        noise = self.model.unet(torch.cat([latents] * 2), t, encoder_hidden_states=context).sample.contiguous()
+        consts = self.scheduler.next_step_constants(t) if is_forward else self.scheduler.prev_step_constants(t)
+        return ops.step_fused(noise, latents.float().contiguous(), consts, g, cfg=True)
+
+    def null_optimization(self, latents, num_inner_steps: int, epsilon: float):
+        """run_videop2p.py:580-612.  Per step: Adam (lr 1e-2 * (1 - i/100)) on the unconditional
+        embedding for up to ``num_inner_steps`` iterations of loss = mse(prev_step(CFG noise), x_prev),
+        early stop at loss < epsilon + i * 2e-5; then one guided DDIM step with the optimised
+        embedding.  The UNet weights are frozen for the duration (the reference's Adam only holds the
+        embedding, so its weight gradients are never used)."""
+        from . import autograd
+        unet = self.model.unet
+        was = [p.requires_grad for p in unet.parameters()]
+        unet.requires_grad_(False)
+        try:
+            uncond, cond = self.context.chunk(2)
+            out = []
+            latent_cur = latents[-1]
+            ts = self.scheduler.timesteps.tolist()
+            self.losses = []
+            for i in range(self.num_ddim_steps):
+                uncond = uncond.clone().detach().float()
+                uncond.requires_grad = True
+                opt = torch.optim.Adam([uncond], lr=1e-2 * (1.0 - i / 100.0))
+                latent_prev = latents[len(latents) - i - 2].float().contiguous()
+                t = ts[i]
+                consts = self.scheduler.prev_step_constants(t)
+                with torch.no_grad():
+                    noise_cond = unet(latent_cur, t, encoder_hidden_states=cond).sample.contiguous()
+                for _ in range(num_inner_steps):
+                    noise_uncond = unet(latent_cur, t, encoder_hidden_states=uncond).sample
+                    loss = autograd.NullTextLoss.apply(noise_uncond, noise_cond, latent_cur.float(), latent_prev,
+                                                       consts, GUIDANCE_SCALE)
+                    opt.zero_grad()
+                    loss.backward()
+                    opt.step()
+                    loss_item = loss.item()
+                    self.losses.append(loss_item)
+                    if loss_item < epsilon + i * 2e-5:
+                        break
+                out.append(uncond[:1].detach())
+                with torch.no_grad():
+                    context = torch.cat([uncond.to(cond.dtype), cond])
+                    latent_cur = self.get_noise_pred(latent_cur, t, False, context)
+            return out
+        finally:
+            for p, r in zip(unet.parameters(), was):
+                p.requires_grad_(r)
+
+    def invert(self, latent: torch.Tensor, prompt: str, num_inner_steps: int = 10, early_stop_epsilon: float = 1e-5,
+               text_embeddings: Optional[torch.Tensor] = None):
+        """Official mode (run_videop2p.py:614-624): DDIM inversion, then null-text optimisation.
+        Returns (latents list, x_T, per-step unconditional embeddings)."""
+        self.init_prompt(prompt, text_embeddings)
+        register_attention_control(self.model, None)
+        lats = self.ddim_loop(latent)
+        unc = self.null_optimization(lats, num_inner_steps, early_stop_epsilon)
+        return lats, lats[-1], unc

@@ -11,8 +11,9 @@ resnet.py:142,158; unet.py:206) are computed on that layout directly.
 Hand-written HIP kernels: the attention layers (K1-K3), the 5-D GroupNorm with the resnet's temb
 add and SiLU fused (K7), LayerNorm (K8) and the GEGLU gate (K9).  Convolutions and projection GEMMs
 stay on MIOpen / hipBLASLt.  When autograd must see an op (the null-text optimisation
-differentiates the UNet w.r.t. the unconditional embedding), the norm / gate ops run as PyTorch
-GPU ops so autograd can trace them.
+differentiates the UNet w.r.t. the unconditional embedding), the same kernels run through the
+autograd wrappers of ``vp2p.autograd``, whose backward passes are HIP kernels too (K1b, K3b, K7b-K9b).
+There is no CPU or PyTorch-op path: the model runs on the GPU only.
 """
 from __future__ import annotations
 
@@ -24,7 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import frame_parallel, ops
+from . import autograd, frame_parallel, ops
 from .attention import CrossAttention, FrameAttention
 
 
@@ -36,50 +37,28 @@ class UNet3DConditionOutput:
         return getattr(self, k)
 
 
-def _kernel_ok(*ts) -> bool:
-    """The K7-K9 kernels are inference-only: use them unless autograd needs to trace this op."""
-    if not ts[0].is_cuda:
-        return False
-    return not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts))
-
-
 def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bool = False,
                       add: Optional[torch.Tensor] = None) -> torch.Tensor:
     """GroupNorm whose statistics span ``frames`` consecutive samples of a ``(b f) c h w``
     channels-last tensor (frames=1: the per-frame GroupNorm of Transformer3DModel.norm), applied
-    to ``x + add[:, :, None, None]`` when ``add`` ((b f), c) is given, then optionally SiLU."""
-    Bf, C, H, W = x.shape
+    to ``x + add[:, :, None, None]`` when ``add`` ((b f), c) is given, then optionally SiLU (K7)."""
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
     shard = frame_parallel.active() if frames > 1 else None
-    if _kernel_ok(x, norm.weight, add) and C % 8 == 0 and x.is_contiguous(memory_format=torch.channels_last):
-        return ops.group_norm(x, norm.num_groups, norm.weight if norm.affine else None,
-                              norm.bias if norm.affine else None, norm.eps, frames, silu=silu,
-                              add=None if add is None else add.contiguous(), shard=shard)
-    if add is not None:
-        x = x + add[:, :, None, None].to(x.dtype)
-    B = Bf // frames
-    G = norm.num_groups
-    xv = x.permute(0, 2, 3, 1).reshape(B, frames * H * W, G, C // G)
-    xf = xv.float()
-    if shard is not None:
-        # statistics span every rank's frames: one all-reduce of (sum x, sum x^2) per norm
-        mean, var = shard.group_norm_stats(xf, frames * H * W * (C // G))
-        mean, var = mean[:, None, :, None], var[:, None, :, None]
-    else:
-        var, mean = torch.var_mean(xf, dim=(1, 3), keepdim=True, unbiased=False)
-    y = (xf - mean) * torch.rsqrt(var + norm.eps)
-    y = y.reshape(Bf, H, W, C)
-    if norm.affine:
-        y = y * norm.weight.float() + norm.bias.float()
-    if silu:
-        y = F.silu(y)
-    return y.to(x.dtype).permute(0, 3, 1, 2)
+    w, b = (norm.weight, norm.bias) if norm.affine else (None, None)
+    add = None if add is None else add.contiguous()
+    if autograd.needs_grad(x, w, b, add):
+        if shard is not None and shard.world > 1:
+            raise NotImplementedError("backward through a frame-sharded GroupNorm (run null-text clip-parallel)")
+        return autograd.GroupNormFn.apply(x, add, w, b, norm.num_groups, norm.eps, frames, silu)
+    return ops.group_norm(x, norm.num_groups, w, b, norm.eps, frames, silu=silu, add=add, shard=shard)
 
 
 def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
     """nn.LayerNorm over channels on K8 (attention.py:200-216)."""
-    if _kernel_ok(x, norm.weight) and x.shape[-1] % 8 == 0 and norm.elementwise_affine:
-        return ops.layer_norm(x, norm.weight, norm.bias, norm.eps)
-    return norm(x)
+    if autograd.needs_grad(x, norm.weight, norm.bias):
+        return autograd.LayerNormFn.apply(x, norm.weight, norm.bias, norm.eps)
+    return ops.layer_norm(x, norm.weight, norm.bias, norm.eps)
 
 
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0) -> torch.Tensor:
@@ -149,10 +128,9 @@ class GEGLU(nn.Module):
 
     def forward(self, x):
         h = self.proj(x)
-        if _kernel_ok(h) and h.shape[-1] % 16 == 0:
-            return ops.geglu(h)
-        a, g = h.chunk(2, dim=-1)
-        return a * F.gelu(g)
+        if autograd.needs_grad(h):
+            return autograd.GEGLUFn.apply(h)
+        return ops.geglu(h)
 
 
 class FeedForward(nn.Module):
