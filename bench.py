@@ -45,6 +45,12 @@ def parse():
     ap.add_argument("--ddim-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-k1-events", action="store_true")
+    ap.add_argument("--mode", default="edit", choices=["edit", "nulltext"],
+                    help="edit: the P2P edit (BASELINE metric, configs[1]); nulltext: official-mode inversion "
+                         "(DDIM inversion + null-text optimisation, configs[3]), one step = one inversion")
+    ap.add_argument("--conv-find", type=int, default=1,
+                    help="1 (default): let MIOpen benchmark its convolution solvers once per shape during warmup (torch.backends.cudnn.benchmark); 0: immediate-mode heuristics")
+    ap.add_argument("--inner-steps", type=int, default=10, help="null-text Adam iterations per DDIM step")
     ap.add_argument("--shard", default="clips", choices=["clips", "frames"],
                     help="clips: every rank edits its own clip (weak scaling, no collective); "
                          "frames: one clip's frames split over the ranks (strong scaling, RCCL)")
@@ -164,6 +170,57 @@ def _cpu_model():
     return "unknown"
 
 
+def nulltext_main(args, world, rank, dev):
+    """configs[3] of BASELINE.json: NullInversion.invert (run_videop2p.py:614-624) of an 8-frame 512^2
+    clip: 50 DDIM-inversion steps, then per step one conditional forward, up to --inner-steps
+    forward+backward Adam iterations (random weights never reach the early-stop epsilon, so always
+    the maximum, the reference's worst case) and one guided step (B=2).  Clip-parallel over ranks."""
+    from vp2p.pipeline import NullInversion, VideoP2PPipeline
+    from vp2p.unet3d import UNet3DConditionModel, init_random_
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    unet = init_random_(UNet3DConditionModel(), seed=0).to(dev, dtype).to(memory_format=torch.channels_last)
+    unet.eval()
+    g = torch.Generator().manual_seed(1)
+    ctx = torch.randn(2, 77, 768, generator=g).to(dev)
+    x0 = torch.randn(1, 4, args.frames, 64, 64, generator=torch.Generator().manual_seed(2 + rank)).to(dev)
+
+    def run(steps):
+        inv = NullInversion(VideoP2PPipeline(unet), num_ddim_steps=steps)
+        return inv.invert(x0, "", num_inner_steps=args.inner_steps, text_embeddings=ctx)
+
+    for _ in range(args.warmup):
+        run(2)
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, x_t, unc = run(args.ddim_steps)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    result = {
+        "metric": "null-text inverted frames/sec (DDIM inversion + null-text optimisation, 512^2)",
+        "value": round(args.frames * args.steps * world / elapsed, 5), "unit": "inverted frames/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (random-init SD-1.5-geometry UNet3D, random text embeddings, x_0~N(0,1))",
+        "config": {"workload": f"official-mode NullInversion.invert, {args.frames} frames 512^2, "
+                               f"{args.ddim_steps} DDIM steps x {args.inner_steps} Adam iterations (max)",
+                   "frames": args.frames, "ddim_steps": args.ddim_steps, "inner_steps": args.inner_steps,
+                   "parallelism": f"clip-parallel x{world}"},
+        "output_finite": bool(torch.isfinite(x_t).all().item()) and all(bool(torch.isfinite(u).all()) for u in unc),
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,6 +232,13 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    torch.backends.cudnn.benchmark = bool(args.conv_find)
+    if args.mode == "nulltext":
+        nulltext_main(args, world, rank, dev)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
 
     import vp2p
     from vp2p import ops

@@ -55,7 +55,10 @@ def test_struct_layout_matches_header(tmp_path):
     from vp2p import _lib
     structs = {"vp2p_frame_attn_args": _lib.FrameAttnArgs, "vp2p_cross_attn_args": _lib.CrossAttnArgs,
                "vp2p_temporal_attn_args": _lib.TemporalAttnArgs, "vp2p_step_args": _lib.StepArgs,
-               "vp2p_group_norm_args": _lib.GroupNormArgs, "vp2p_layer_norm_args": _lib.LayerNormArgs}
+               "vp2p_group_norm_args": _lib.GroupNormArgs, "vp2p_layer_norm_args": _lib.LayerNormArgs,
+               "vp2p_frame_attn_bwd_args": _lib.FrameAttnBwdArgs,
+               "vp2p_temporal_attn_bwd_args": _lib.TemporalAttnBwdArgs,
+               "vp2p_nulltext_loss_args": _lib.NullTextLossArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

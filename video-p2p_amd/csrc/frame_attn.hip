@@ -441,7 +441,219 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2(const vp2p_frame_
   }
 }
 
-static int k1_variant() {  // VP2P_K1_VARIANT=0 forces the one-set kernel (A/B experiments)
+// ------------------------------------------------------------------------------------------------
+// v3: bf16, d = 40 (the res-64 layers, 88% of the FLOPs).  Two changes over frame_attn_kernel_x2:
+//  * the running max is folded into the QK^T MFMA.  d = 40 pads to a 48-wide K-dim, so K carries a
+//    constant 1 in column 40 and Q (pre-scaled by scale*log2 e) carries -m in that column: the MFMA
+//    returns s*scale*log2e - m directly and p = exp2(acc) is ONE VALU op per score (no fma).  m is
+//    kept as a bf16 value (exact in the MFMA); softmax is invariant to it, so its rounding does not
+//    matter, only the lazy-rescale bound does.  The per-block max is only needed to detect the rare
+//    case "some score exceeds m + kRescaleThr" (one v_max3 chain + one wave vote, no cross-lane
+//    exchange); then m moves, O (and its ones-row sum) is rescaled and Q's column 40 is rewritten.
+//  * K/V tiles stream global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no compiler
+//    vmcnt(0) before the first MFMA of a tile), double buffered, one barrier per 128-key tile.  The
+//    LDS image is plane-major: plane c holds 16-byte piece c (8 channels) of every key, planes
+//    2112 B apart (16 banks), so K row reads (ds_read_b128) and V^T transposed reads
+//    (ds_read_b64_tr_b16) are both conflict-free.  Constant planes supply K's column 40 (= 1), V's
+//    ones row (d = 40, the row sum rides in the PV MFMA) and V's zero rows 41..63.
+// ------------------------------------------------------------------------------------------------
+namespace k1v3 {
+constexpr int D = 40;
+constexpr int KT = 128;                    // keys per tile
+constexpr int CSTRIDE = KT * 16 + 64;      // bytes per plane (+64 B: consecutive planes 16 banks apart)
+constexpr int KPL = 6;                     // K planes: d 0..39 + [1, 0 x 7]
+constexpr int VPL = 8;                     // V planes: d 0..39 + [1, 0 x 7] + 2 zero planes (d 48..63)
+constexpr int KBYTES = KPL * CSTRIDE, VBYTES = VPL * CSTRIDE;
+constexpr int BUF = KBYTES + VBYTES;
+constexpr int LDS_BYTES = 2 * BUF;
+constexpr int DATA_PL = D / 8;             // 5 planes loaded per tile
+}  // namespace k1v3
+
+__device__ __forceinline__ bf16x8 vt_frag_planes(const char* vbuf, int key0, int sp, int t) {
+  const int l = lane_id();
+  const int h = l >> 5, g = (l >> 4) & 1, q = (l >> 2) & 3, p = l & 3;
+  const int c0 = 32 * t + 16 * g + 4 * p;
+  const char* base = vbuf + (c0 >> 3) * k1v3::CSTRIDE + (c0 & 7) * 2 + (key0 + 16 * sp + 4 * h + q) * 16;
+  const bf16x4 lo = lds_read_tr(reinterpret_cast<const bf16*>(base));
+  const bf16x4 hi = lds_read_tr(reinterpret_cast<const bf16*>(base + 8 * 16));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+template <int UNR>
+__global__ __launch_bounds__(256, 2) void frame_attn_kernel_v3(const vp2p_frame_attn_args a) {
+  using namespace k1v3;
+  using M = Mfma<bf16>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int FQ = a.frames * a.tokens_q;
+  const int qblocks = (FQ + 255) >> 8;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = bid / qblocks, qb = bid - bh * qblocks;
+  const int b = bh / a.heads, head = bh - b * a.heads;
+  const int Nk = a.tokens_kv;
+  const float cs = a.scale * kLog2e;
+
+  // constant planes of both stages: K plane 5 / V plane 5 = [1, 0 x 7] per key, V planes 6, 7 = 0
+  for (int i = tid; i < 2 * KT; i += 256) {
+    char* st = smem + (i >= KT ? BUF : 0);
+    const int k = i & (KT - 1);
+    const u32x4 one = {0x3F80u, 0u, 0u, 0u};
+    *reinterpret_cast<u32x4*>(st + 5 * CSTRIDE + k * 16) = one;
+    *reinterpret_cast<u32x4*>(st + KBYTES + 5 * CSTRIDE + k * 16) = one;
+    *reinterpret_cast<u32x4*>(st + KBYTES + 6 * CSTRIDE + k * 16) = u32x4{0, 0, 0, 0};
+    *reinterpret_cast<u32x4*>(st + KBYTES + 7 * CSTRIDE + k * 16) = u32x4{0, 0, 0, 0};
+  }
+
+  const bf16* kbase = static_cast<const bf16*>(a.k) + (int64_t)b * a.k_sb + head * D;
+  const bf16* vbase = static_cast<const bf16*>(a.v) + (int64_t)b * a.v_sb + head * D;
+  // one tile = 2 tensors x 5 planes x 2 halves of 64 keys = 20 wave-wide DMA pieces, 5 per wave
+  auto issue_tile = [&](int kt, int stage) {
+    char* st = smem + stage * BUF;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int id = w + 4 * j;
+      const int x = id >= 10 ? 1 : 0, rem = id - 10 * x, c = rem >> 1, hf = rem & 1;
+      int key = kt + hf * 64 + l;
+      key = key < Nk ? key : Nk - 1;                      // clamp: those keys are masked
+      const bf16* src = (x ? vbase + (int64_t)key * a.v_sn : kbase + (int64_t)key * a.k_sn) + c * 8;
+      char* dst = st + (x ? KBYTES : 0) + c * CSTRIDE + hf * 1024;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  issue_tile(0, 0);
+
+  int qi[2], fr[2], pos[2];
+  bool qv[2];
+  bf16x8 qf[2][3];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    qi[st] = qb * 256 + w * 64 + st * 32 + r;
+    qv[st] = qi[st] < FQ;
+    fr[st] = qv[st] ? qi[st] / a.tokens_q : 0;
+    pos[st] = qv[st] ? qi[st] - fr[st] * a.tokens_q : 0;
+    const bf16* qrow = static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)fr[st] * a.q_sf +
+                       (int64_t)pos[st] * a.q_sn + head * D;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      bf16x8 f = qv[st] ? M::row_frag(qrow, s, h, D) : M::zero();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (bf16)((float)f[j] * cs);
+      qf[st][s] = f;                                       // s = 2, h = 1: column 40 = -m = 0 for now
+    }
+  }
+  float m[2] = {0.f, 0.f};                                 // the (bf16-exact) max in Q's column 40
+  f32x16 o[2][2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) o[st][0] = o[st][1] = zero16();
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  auto compute_tile = [&](const char* kb, const char* vb, int kt, auto masked_tag) {
+    constexpr bool MASKED = decltype(masked_tag)::value;
+#pragma unroll UNR
+    for (int key0 = 0; key0 < KT; key0 += 32) {
+      if (MASKED && kt + key0 >= Nk) break;
+      f32x16 s[2] = {zero16(), zero16()};
+#pragma unroll
+      for (int si = 0; si < 3; ++si) {
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kb + (2 * si + h) * CSTRIDE + (key0 + r) * 16);
+        s[0] = M::mma(ka, qf[0][si], s[0]);
+        s[1] = M::mma(ka, qf[1][si], s[1]);
+      }
+      float mx[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        if constexpr (MASKED) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (kt + key0 + acc_row(i, h) >= Nk) s[st][i] = kNegInf;
+        }
+        float v = fmaxf(s[st][0], s[st][1]);
+#pragma unroll
+        for (int i = 2; i < 16; i += 2) v = fmaxf(v, fmaxf(s[st][i], s[st][i + 1]));
+        mx[st] = v;
+      }
+      const bool first = kt == 0 && key0 == 0;
+      if (first || __any(mx[0] > kRescaleThr || mx[1] > kRescaleThr)) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const float rm = fmaxf(mx[st], xhalf(mx[st]));  // row max relative to the current m
+          if (first || rm > kRescaleThr) {
+            const bf16 mb = (bf16)(m[st] + rm);
+            const float delta = (float)mb - m[st];
+            const float alpha = fast_exp2(-delta);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) o[st][t][i] *= alpha;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[st][i] -= delta;
+            m[st] = (float)mb;
+            if (h) qf[st][2][0] = -mb;
+          }
+        }
+      }
+      bf16x8 pf[2][2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[st][i] = fast_exp2(s[st][i]);
+        pf[st][0] = M::p_frag(s[st], 0);
+        pf[st][1] = M::p_frag(s[st], 1);
+      }
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 vf = vt_frag_planes(vb, key0, sp, t);
+          o[0][t] = M::mma(vf, pf[0][sp], o[0][t]);
+          o[1][t] = M::mma(vf, pf[1][sp], o[1][t]);
+        }
+    }
+  };
+
+  int stage = 0;
+  for (int kt = 0; kt < Nk; kt += KT) {
+    if (kt + KT < Nk) issue_tile(kt + KT, stage ^ 1);
+    const char* kb = smem + stage * BUF;
+    if (kt + KT <= Nk) compute_tile(kb, kb + KBYTES, kt, std::false_type{});
+    else compute_tile(kb, kb + KBYTES, kt, std::true_type{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stage ^= 1;
+  }
+
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const float mine = o[st][1][4];                        // O^T row 40 = the ones row: lanes h = 0, reg 4
+    const float other = xhalf(mine);                       // all 64 lanes take part in the swap
+    const float lrow = h == 0 ? mine : other;
+    if (a.lse && qv[st]) a.lse[(int64_t)(b * a.heads + head) * FQ + qi[st]] = m[st] + log2f(lrow);
+    if (qv[st]) {
+      const float inv = 1.f / lrow;
+      bf16* orow = static_cast<bf16*>(a.o) + (int64_t)b * a.o_sb + (int64_t)fr[st] * a.o_sf +
+                   (int64_t)pos[st] * a.o_sn + head * D;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dc = 32 * t + 8 * g + 4 * h;
+          if (dc < D) {
+            bf16x4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[st][t][4 * g + j] * inv);
+            *reinterpret_cast<bf16x4*>(orow + dc) = v;
+          }
+        }
+    }
+  }
+}
+
+static int k1_variant() {  // VP2P_K1_VARIANT=0 / 2 force the one-set / x2 kernels (A/B experiments)
   const char* e = getenv("VP2P_K1_VARIANT");
   return e ? atoi(e) : 2;
 }
@@ -450,8 +662,20 @@ template <typename T, int D>
 static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
   using C = FrameCfg<T, D>;
   const int FQ = a->frames * a->tokens_q;
+  if constexpr (C::BF && D == k1v3::D) {
+    const int var = k1_variant();
+    if (var == 3 || var == 4) {
+      const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
+      if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+      if (var == 3)
+        hipLaunchKernelGGL(frame_attn_kernel_v3<4>, dim3((unsigned)nwg), dim3(256), k1v3::LDS_BYTES, stream, *a);
+      else
+        hipLaunchKernelGGL(frame_attn_kernel_v3<1>, dim3((unsigned)nwg), dim3(256), k1v3::LDS_BYTES, stream, *a);
+      return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+    }
+  }
   if constexpr (C::BF && C::ONES && D <= 64) {
-    if (k1_variant() == 2) {
+    if (k1_variant() >= 2) {
       const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
       if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
       hipLaunchKernelGGL((frame_attn_kernel_x2<D>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);

@@ -534,18 +534,32 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_kernel(const vp2p_group_norm
   const int C = a.channels, G = a.groups, R = g.R, nvec = g.nvec, cg = g.cg;
   const int b = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
   gn_group_stats(a, g, partials, nsets, b, s_w, s_mean, s_rstd, s_n);
-  if (tid < G) {
+  {  // tpg threads per group sum a strided share of the (set, part) partials, then one add per group
+    const int tpg = g.threads / G;
+    const int gi = tid / tpg, k = tid - gi * tpg;
     float u1 = 0.f, u2 = 0.f;
-    for (int set = 0; set < bsets; ++set)
-      for (int p = 0; p < g.parts; ++p) {
-        const float* q = bpart + ((((int64_t)set * a.batch + b) * g.parts + p) * G + tid) * 2;
+    if (gi < G) {
+      for (int e = k; e < bsets * g.parts; e += tpg) {
+        const int set = e / g.parts, p = e - set * g.parts;
+        const float* q = bpart + ((((int64_t)set * a.batch + b) * g.parts + p) * G + gi) * 2;
         u1 += q[0];
         u2 += q[1];
       }
-    s_m1[tid] = u1 / s_n[tid];
-    s_m2[tid] = u2 / s_n[tid];
+    }
+    s_w[tid] = u1;
+    s_w[512 + tid] = u2;
+    __syncthreads();
+    if (tid < G) {
+      float v1 = 0.f, v2 = 0.f;
+      for (int e = 0; e < tpg; ++e) {
+        v1 += s_w[tid * tpg + e];
+        v2 += s_w[512 + tid * tpg + e];
+      }
+      s_m1[tid] = v1 / s_n[tid];
+      s_m2[tid] = v2 / s_n[tid];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const int v = tid % nvec, r = tid / nvec;
   float mu[8], rs[8], wt[8], bs[8], m1[8], m2[8];
 #pragma unroll
