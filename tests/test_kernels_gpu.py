@@ -77,6 +77,42 @@ def test_frame_attention_large_logits():
     assert _rel(_np(out), ref) < 1e-4
 
 
+@pytest.mark.parametrize("spike", [4.0, 12.0, "overflow"])
+def test_frame_attention_bf16_spikes(spike):
+    """bf16 d=40 (the x2f kernel): a late key whose logits jump far above the first block's max.
+    4x / 12x exercise the row-sum rescale; "overflow" aligns the key with one query so that its logit
+    is ~100 nats above the running max (p would overflow bf16/fp32), forcing the exact per-row
+    fallback.  Tolerance: the bf16 bar of the north star, 2e-2 of max|ref|."""
+    from vp2p import ops
+    heads, B, frames, n, d = 8, 1, 2, 512, 40
+    C = heads * d
+    q = _rand((B * frames, n, C), 4, 1.0)
+    k = _rand((B * frames, n, C), 5, 1.0)
+    if spike == "overflow":
+        k[0, 450, :d] = 16.0 * q[1, 100, :d]
+        k[0, 300, d:2 * d] = 12.0 * q[0, 7, d:2 * d]
+    else:
+        k[0, 450] *= spike
+    v = _rand((B * frames, n, C), 6, 1.0)
+    q, k, v = (x.to(torch.bfloat16) for x in (q, k, v))
+    ref = O.frame_attention(_np(q), _np(k), _np(v), frames, heads)
+    assert np.isfinite(ref).all()
+    out = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads)
+    lse = torch.empty(B * heads, frames * n, device=DEV)
+    out2 = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, lse=lse)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+    assert _rel(_np(out), ref) < 2e-2, _rel(_np(out), ref)
+    assert torch.equal(out, out2)
+    # log-sum-exp (log2 units, scale folded in) against float64
+    qd = _np(q).astype(np.float64).reshape(B, frames * n, heads, d).transpose(0, 2, 1, 3)
+    kd = _np(k).astype(np.float64).reshape(B, frames, n, heads, d)[:, 0].transpose(0, 2, 1, 3)
+    sc = qd @ kd.transpose(0, 1, 3, 2) * d ** -0.5 * np.log2(np.e)
+    mx = sc.max(-1, keepdims=True)
+    lse_ref = (mx[..., 0] + np.log2(np.exp2(sc - mx).sum(-1))).reshape(B * heads, frames * n)
+    assert np.abs(lse.cpu().numpy() - lse_ref).max() < 5e-2
+
+
 # ------------------------------------------------------------------------------------------------
 def _controller(tokenizer, name, step):
     import spec

@@ -6,7 +6,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "video-p2p_amd"))
 from vp2p import ops  # noqa: E402
 
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "2,3").split(",")]
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "2,4").split(",")]
 B, f, heads = 4, 8, 8
 for hw, C in ((4096, 320), (1024, 640)):
     q = torch.randn(B * f, hw, C, device="cuda", dtype=torch.bfloat16)

@@ -442,51 +442,74 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2(const vp2p_frame_
 }
 
 // ------------------------------------------------------------------------------------------------
-// v3: bf16, d = 40 (the res-64 layers, 88% of the FLOPs).  Two changes over frame_attn_kernel_x2:
-//  * the running max is folded into the QK^T MFMA.  d = 40 pads to a 48-wide K-dim, so K carries a
-//    constant 1 in column 40 and Q (pre-scaled by scale*log2 e) carries -m in that column: the MFMA
-//    returns s*scale*log2e - m directly and p = exp2(acc) is ONE VALU op per score (no fma).  m is
-//    kept as a bf16 value (exact in the MFMA); softmax is invariant to it, so its rounding does not
-//    matter, only the lazy-rescale bound does.  The per-block max is only needed to detect the rare
-//    case "some score exceeds m + kRescaleThr" (one v_max3 chain + one wave vote, no cross-lane
-//    exchange); then m moves, O (and its ones-row sum) is rescaled and Q's column 40 is rewritten.
-//  * K/V tiles stream global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no compiler
-//    vmcnt(0) before the first MFMA of a tile), double buffered, one barrier per 128-key tile.  The
-//    LDS image is plane-major: plane c holds 16-byte piece c (8 channels) of every key, planes
-//    2112 B apart (16 banks), so K row reads (ds_read_b128) and V^T transposed reads
-//    (ds_read_b64_tr_b16) are both conflict-free.  Constant planes supply K's column 40 (= 1), V's
-//    ones row (d = 40, the row sum rides in the PV MFMA) and V's zero rows 41..63.
+// x2f: bf16, d <= 64 with a spare V^T row (d = 40, the res-64 layers, 88% of the FLOPs).
+// frame_attn_kernel_x2 with the inner 128-key tile made one straight-line, software-pipelined block:
+//  * no per-score max: m starts at the exact row max of the first 32-key block; afterwards growth
+//    is read off the ones-row sum (O^T row D) once per tile: if the tile's sum dl = l - l_prev
+//    exceeds kSumThr, m moves up by log2(dl) (so the tile's largest p is <= 1 again) and O and l
+//    are rescaled.  P is bf16 and O/l fp32, so between checks p up to 2^127 is still exact to
+//    rounding; only a score more than 127 log2 units (88 nats) above the running max overflows,
+//    and a row whose final sum is not finite is recomputed exactly by a per-lane two-pass path
+//    at the end (never taken on real data; forced by a test);
+//  * with no branch inside a tile, QK^T of block j+1 is issued before the exp2/cvt of block j, so
+//    the VALU softmax of one block runs under the MFMAs of the next (T15 "att[2]").
 // ------------------------------------------------------------------------------------------------
-namespace k1v3 {
-constexpr int D = 40;
-constexpr int KT = 128;                    // keys per tile
-constexpr int CSTRIDE = KT * 16 + 64;      // bytes per plane (+64 B: consecutive planes 16 banks apart)
-constexpr int KPL = 6;                     // K planes: d 0..39 + [1, 0 x 7]
-constexpr int VPL = 8;                     // V planes: d 0..39 + [1, 0 x 7] + 2 zero planes (d 48..63)
-constexpr int KBYTES = KPL * CSTRIDE, VBYTES = VPL * CSTRIDE;
-constexpr int BUF = KBYTES + VBYTES;
-constexpr int LDS_BYTES = 2 * BUF;
-constexpr int DATA_PL = D / 8;             // 5 planes loaded per tile
-}  // namespace k1v3
+constexpr float kSumThr = 4096.f;
 
-__device__ __forceinline__ bf16x8 vt_frag_planes(const char* vbuf, int key0, int sp, int t) {
-  const int l = lane_id();
-  const int h = l >> 5, g = (l >> 4) & 1, q = (l >> 2) & 3, p = l & 3;
-  const int c0 = 32 * t + 16 * g + 4 * p;
-  const char* base = vbuf + (c0 >> 3) * k1v3::CSTRIDE + (c0 & 7) * 2 + (key0 + 16 * sp + 4 * h + q) * 16;
-  const bf16x4 lo = lds_read_tr(reinterpret_cast<const bf16*>(base));
-  const bf16x4 hi = lds_read_tr(reinterpret_cast<const bf16*>(base + 8 * 16));
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
+// Exact two-pass softmax row of one query in plain fp32 VALU (the overflow fallback of x2f):
+// writes this lane's epilogue slots of the output row and the row's log-sum-exp.
+template <int D>
+__device__ __forceinline__ void frame_attn_exact_row(const vp2p_frame_attn_args& a, int b, int head, int fr,
+                                                     int pos, int64_t qi, int h, float cs) {
+  const bf16* qrow = static_cast<const bf16*>(a.q) + b * a.q_sb + (int64_t)fr * a.q_sf + (int64_t)pos * a.q_sn + head * D;
+  const bf16* kb = static_cast<const bf16*>(a.k) + b * a.k_sb + head * D;
+  const bf16* vb = static_cast<const bf16*>(a.v) + b * a.v_sb + head * D;
+  float qv[D], acc[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) { qv[c] = (float)qrow[c]; acc[c] = 0.f; }
+  float mx = kNegInf;
+  for (int key = 0; key < a.tokens_kv; ++key) {
+    const bf16* kr = kb + (int64_t)key * a.k_sn;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) s = __builtin_fmaf(qv[c], (float)kr[c], s);
+    mx = fmaxf(mx, s * cs);
+  }
+  float l = 0.f;
+  for (int key = 0; key < a.tokens_kv; ++key) {
+    const bf16* kr = kb + (int64_t)key * a.k_sn;
+    const bf16* vr = vb + (int64_t)key * a.v_sn;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) s = __builtin_fmaf(qv[c], (float)kr[c], s);
+    const float p = exp2f(__builtin_fmaf(s, cs, -mx));
+    l += p;
+#pragma unroll
+    for (int c = 0; c < D; ++c) acc[c] = __builtin_fmaf(p, (float)vr[c], acc[c]);
+  }
+  const int FQ = a.frames * a.tokens_q;
+  if (a.lse) a.lse[(int64_t)(b * a.heads + head) * FQ + qi] = mx + log2f(l);
+  const float inv = 1.f / l;
+  bf16* orow = static_cast<bf16*>(a.o) + b * a.o_sb + (int64_t)fr * a.o_sf + (int64_t)pos * a.o_sn + head * D;
+#pragma unroll
+  for (int dc = 0; dc < D; dc += 8) {
+    bf16x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (bf16)((h ? acc[dc + 4 + j] : acc[dc + j]) * inv);
+    *reinterpret_cast<bf16x4*>(orow + dc + 4 * h) = v;
+  }
 }
 
-template <int UNR>
-__global__ __launch_bounds__(256, 2) void frame_attn_kernel_v3(const vp2p_frame_attn_args a) {
-  using namespace k1v3;
-  using M = Mfma<bf16>;
+template <int D>
+__global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame_attn_args a) {
+  using T = bf16;
+  using M = Mfma<T>;
+  using C = FrameCfg<T, D>;
+  static_assert(C::ONES && D <= 64 && D % 8 == 0, "x2f: bf16, spare ones row");
+  constexpr int NBLK = C::KT / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Ks = reinterpret_cast<T*>(smem);
+  T* Vs = Ks + C::KT * C::KROW;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int FQ = a.frames * a.tokens_q;
   const int qblocks = (FQ + 255) >> 8;
@@ -496,75 +519,93 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_v3(const vp2p_frame_
   const int Nk = a.tokens_kv;
   const float cs = a.scale * kLog2e;
 
-  // constant planes of both stages: K plane 5 / V plane 5 = [1, 0 x 7] per key, V planes 6, 7 = 0
-  for (int i = tid; i < 2 * KT; i += 256) {
-    char* st = smem + (i >= KT ? BUF : 0);
-    const int k = i & (KT - 1);
-    const u32x4 one = {0x3F80u, 0u, 0u, 0u};
-    *reinterpret_cast<u32x4*>(st + 5 * CSTRIDE + k * 16) = one;
-    *reinterpret_cast<u32x4*>(st + KBYTES + 5 * CSTRIDE + k * 16) = one;
-    *reinterpret_cast<u32x4*>(st + KBYTES + 6 * CSTRIDE + k * 16) = u32x4{0, 0, 0, 0};
-    *reinterpret_cast<u32x4*>(st + KBYTES + 7 * CSTRIDE + k * 16) = u32x4{0, 0, 0, 0};
-  }
-
-  const bf16* kbase = static_cast<const bf16*>(a.k) + (int64_t)b * a.k_sb + head * D;
-  const bf16* vbase = static_cast<const bf16*>(a.v) + (int64_t)b * a.v_sb + head * D;
-  // one tile = 2 tensors x 5 planes x 2 halves of 64 keys = 20 wave-wide DMA pieces, 5 per wave
-  auto issue_tile = [&](int kt, int stage) {
-    char* st = smem + stage * BUF;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int id = w + 4 * j;
-      const int x = id >= 10 ? 1 : 0, rem = id - 10 * x, c = rem >> 1, hf = rem & 1;
-      int key = kt + hf * 64 + l;
-      key = key < Nk ? key : Nk - 1;                      // clamp: those keys are masked
-      const bf16* src = (x ? vbase + (int64_t)key * a.v_sn : kbase + (int64_t)key * a.k_sn) + c * 8;
-      char* dst = st + (x ? KBYTES : 0) + c * CSTRIDE + hf * 1024;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-    }
-  };
-  issue_tile(0, 0);
-
   int qi[2], fr[2], pos[2];
   bool qv[2];
-  bf16x8 qf[2][3];
+  bf16x8 qf[2][C::KS];
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
     qi[st] = qb * 256 + w * 64 + st * 32 + r;
     qv[st] = qi[st] < FQ;
     fr[st] = qv[st] ? qi[st] / a.tokens_q : 0;
     pos[st] = qv[st] ? qi[st] - fr[st] * a.tokens_q : 0;
-    const bf16* qrow = static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)fr[st] * a.q_sf +
-                       (int64_t)pos[st] * a.q_sn + head * D;
+    const T* qrow = static_cast<const T*>(a.q) + b * a.q_sb + fr[st] * a.q_sf + pos[st] * a.q_sn + head * D;
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      bf16x8 f = qv[st] ? M::row_frag(qrow, s, h, D) : M::zero();
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = (bf16)((float)f[j] * cs);
-      qf[st][s] = f;                                       // s = 2, h = 1: column 40 = -m = 0 for now
-    }
+    for (int s = 0; s < C::KS; ++s) qf[st][s] = qv[st] ? M::row_frag(qrow, s, h, D) : M::zero();
   }
-  float m[2] = {0.f, 0.f};                                 // the (bf16-exact) max in Q's column 40
-  f32x16 o[2][2];
-#pragma unroll
-  for (int st = 0; st < 2; ++st) o[st][0] = o[st][1] = zero16();
-
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int i = tid; i < C::LDS_BYTES / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0, 0, 0, 0};
   __syncthreads();
+  for (int k = tid; k < C::KT; k += 256) Vs[k * C::VROW + D] = (T)1.0f;   // O^T row D = sum_k p
 
-  auto compute_tile = [&](const char* kb, const char* vb, int kt, auto masked_tag) {
-    constexpr bool MASKED = decltype(masked_tag)::value;
-#pragma unroll UNR
-    for (int key0 = 0; key0 < KT; key0 += 32) {
-      if (MASKED && kt + key0 >= Nk) break;
-      f32x16 s[2] = {zero16(), zero16()};
+  const T* kbase = static_cast<const T*>(a.k) + b * a.k_sb + head * D;
+  const T* vbase = static_cast<const T*>(a.v) + b * a.v_sb + head * D;
+  u32x4 kreg[C::NCH], vreg[C::NCH];
+  auto load_tile = [&](int kt) {
 #pragma unroll
-      for (int si = 0; si < 3; ++si) {
-        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kb + (2 * si + h) * CSTRIDE + (key0 + r) * 16);
-        s[0] = M::mma(ka, qf[0][si], s[0]);
-        s[1] = M::mma(ka, qf[1][si], s[1]);
+    for (int i = 0; i < C::NCH; ++i) {
+      const int c = tid + i * 256;
+      const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
+      const int key = kt + row;
+      if (c < C::KT * C::CPR && key < Nk) {
+        kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)key * a.k_sn + col);
+        vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (int64_t)key * a.v_sn + col);
+      } else {
+        kreg[i] = u32x4{0, 0, 0, 0};
+        vreg[i] = u32x4{0, 0, 0, 0};
       }
-      float mx[2];
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < C::NCH; ++i) {
+      const int c = tid + i * 256;
+      if (c < C::KT * C::CPR) {
+        const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
+        *reinterpret_cast<u32x4*>(Ks + row * C::KROW + col) = kreg[i];
+        *reinterpret_cast<u32x4*>(Vs + row * C::VROW + col) = vreg[i];
+      }
+    }
+  };
+
+  float m[2] = {0.f, 0.f}, lp[2] = {0.f, 0.f};
+  f32x16 o[2][C::NT];
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t) o[st][t] = zero16();
+
+  // m starts at the exact row max of keys 0..31 (tile 0 in LDS; ragged Nk < 32 masked)
+  auto init_max = [&]() {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f32x16 s = zero16();
+#pragma unroll
+      for (int si = 0; si < C::KS; ++si)
+        s = M::mma(*reinterpret_cast<const bf16x8*>(Ks + r * C::KROW + 16 * si + 8 * h), qf[st][si], s);
+      float v = kNegInf;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v = fmaxf(v, acc_row(i, h) < Nk ? s[i] : kNegInf);
+      m[st] = fmaxf(v, xhalf(v)) * cs;
+    }
+  };
+
+  auto compute_tile = [&](int kt, auto masked_tag) {
+    constexpr bool MASKED = decltype(masked_tag)::value;
+#pragma unroll
+    for (int j = 0; j < NBLK; ++j) {
+      const int key0 = 32 * j;
+      if (MASKED && kt + key0 >= Nk) break;
+      // set 0's QK^T, then set 1's: set 0's softmax runs while set 1's MFMAs execute, and set 1's
+      // softmax while set 0's PV MFMAs execute
+      f32x16 s[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        s[st] = zero16();
+#pragma unroll
+        for (int si = 0; si < C::KS; ++si) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ks + (key0 + r) * C::KROW + 16 * si + 8 * h);
+          s[st] = M::mma(af, qf[st][si], s[st]);
+        }
+      }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         if constexpr (MASKED) {
@@ -572,73 +613,70 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_v3(const vp2p_frame_
           for (int i = 0; i < 16; ++i)
             if (kt + key0 + acc_row(i, h) >= Nk) s[st][i] = kNegInf;
         }
-        float v = fmaxf(s[st][0], s[st][1]);
+        const float nm = -m[st];
 #pragma unroll
-        for (int i = 2; i < 16; i += 2) v = fmaxf(v, fmaxf(s[st][i], s[st][i + 1]));
-        mx[st] = v;
+        for (int i = 0; i < 16; ++i) s[st][i] = fast_exp2(__builtin_fmaf(s[st][i], cs, nm));
+        const bf16x8 p0 = M::p_frag(s[st], 0), p1 = M::p_frag(s[st], 1);
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t) o[st][t] = M::mma(vt_frag_lds<C::VROW>(Vs, key0, 0, t), p0, o[st][t]);
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t) o[st][t] = M::mma(vt_frag_lds<C::VROW>(Vs, key0, 1, t), p1, o[st][t]);
       }
-      const bool first = kt == 0 && key0 == 0;
-      if (first || __any(mx[0] > kRescaleThr || mx[1] > kRescaleThr)) {
+    }
+    // once per tile: the tile's row sum (valid on lanes h == ONE_H; the other half reads a zero row)
+    float lc[2];
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const float rm = fmaxf(mx[st], xhalf(mx[st]));  // row max relative to the current m
-          if (first || rm > kRescaleThr) {
-            const bf16 mb = (bf16)(m[st] + rm);
-            const float delta = (float)mb - m[st];
-            const float alpha = fast_exp2(-delta);
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-              for (int i = 0; i < 16; ++i) o[st][t][i] *= alpha;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) s[st][i] -= delta;
-            m[st] = (float)mb;
-            if (h) qf[st][2][0] = -mb;
-          }
-        }
-      }
-      bf16x8 pf[2][2];
+    for (int st = 0; st < 2; ++st) lc[st] = o[st][C::ONE_T][C::ONE_I];
+    if (__any(lc[0] - lp[0] > kSumThr || lc[1] - lp[1] > kSumThr)) {
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
+        const float mine = lc[st] - lp[st];
+        const float other = xhalf(mine);
+        const float dl = h == C::ONE_H ? mine : other;
+        const float delta = dl > kSumThr ? __log2f(dl) : 0.f;   // rows that did not grow: alpha = 1
+        const float alpha = fast_exp2(-delta);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[st][i] = fast_exp2(s[st][i]);
-        pf[st][0] = M::p_frag(s[st], 0);
-        pf[st][1] = M::p_frag(s[st], 1);
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[st][t][i] *= alpha;
+        lc[st] *= alpha;
+        m[st] += delta;
       }
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const bf16x8 vf = vt_frag_planes(vb, key0, sp, t);
-          o[0][t] = M::mma(vf, pf[0][sp], o[0][t]);
-          o[1][t] = M::mma(vf, pf[1][sp], o[1][t]);
-        }
     }
+    lp[0] = lc[0];
+    lp[1] = lc[1];
   };
 
-  int stage = 0;
-  for (int kt = 0; kt < Nk; kt += KT) {
-    if (kt + KT < Nk) issue_tile(kt + KT, stage ^ 1);
-    const char* kb = smem + stage * BUF;
-    if (kt + KT <= Nk) compute_tile(kb, kb + KBYTES, kt, std::false_type{});
-    else compute_tile(kb, kb + KBYTES, kt, std::true_type{});
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  load_tile(0);
+  int kt = 0;
+  for (; kt + C::KT <= Nk; kt += C::KT) {
     __syncthreads();
-    stage ^= 1;
+    store_tile();
+    __syncthreads();
+    if (kt + C::KT < Nk) load_tile(kt + C::KT);
+    if (kt == 0) init_max();
+    compute_tile(kt, std::false_type{});
   }
-
+  if (kt < Nk) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (kt == 0) init_max();
+    compute_tile(kt, std::true_type{});
+  }
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
-    const float mine = o[st][1][4];                        // O^T row 40 = the ones row: lanes h = 0, reg 4
-    const float other = xhalf(mine);                       // all 64 lanes take part in the swap
-    const float lrow = h == 0 ? mine : other;
-    if (a.lse && qv[st]) a.lse[(int64_t)(b * a.heads + head) * FQ + qi[st]] = m[st] + log2f(lrow);
-    if (qv[st]) {
+    const float mine = o[st][C::ONE_T][C::ONE_I];
+    const float other = xhalf(mine);
+    const float lrow = (h == C::ONE_H) ? mine : other;
+    // inf / NaN by exponent bits (the file builds with -fno-honor-nans)
+    const bool bad = qv[st] && (__float_as_uint(lrow) & 0x7f800000u) == 0x7f800000u;
+    if (qv[st] && !bad) {
+      if (a.lse) a.lse[(int64_t)(b * a.heads + head) * FQ + qi[st]] = m[st] + log2f(lrow);
       const float inv = 1.f / lrow;
-      bf16* orow = static_cast<bf16*>(a.o) + (int64_t)b * a.o_sb + (int64_t)fr[st] * a.o_sf +
-                   (int64_t)pos[st] * a.o_sn + head * D;
+      T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr[st] * a.o_sf + pos[st] * a.o_sn + head * D;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < C::NT; ++t)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int dc = 32 * t + 8 * g + 4 * h;
@@ -650,27 +688,24 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_v3(const vp2p_frame_
           }
         }
     }
+    if (bad) frame_attn_exact_row<D>(a, b, head, fr[st], pos[st], qi[st], h, cs);
   }
 }
 
-static int k1_variant() {  // VP2P_K1_VARIANT=0 / 2 force the one-set / x2 kernels (A/B experiments)
+static int k1_variant() {  // VP2P_K1_VARIANT=0 / 2 / 4 force the one-set / x2 / x2f kernels (A/B experiments)
   const char* e = getenv("VP2P_K1_VARIANT");
-  return e ? atoi(e) : 2;
+  return e ? atoi(e) : 4;
 }
 
 template <typename T, int D>
 static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
   using C = FrameCfg<T, D>;
   const int FQ = a->frames * a->tokens_q;
-  if constexpr (C::BF && D == k1v3::D) {
-    const int var = k1_variant();
-    if (var == 3 || var == 4) {
+  if constexpr (C::BF && C::ONES && D <= 64) {
+    if (k1_variant() >= 4) {
       const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
       if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-      if (var == 3)
-        hipLaunchKernelGGL(frame_attn_kernel_v3<4>, dim3((unsigned)nwg), dim3(256), k1v3::LDS_BYTES, stream, *a);
-      else
-        hipLaunchKernelGGL(frame_attn_kernel_v3<1>, dim3((unsigned)nwg), dim3(256), k1v3::LDS_BYTES, stream, *a);
+      hipLaunchKernelGGL((frame_attn_kernel_x2f<D>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);
       return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
     }
   }
