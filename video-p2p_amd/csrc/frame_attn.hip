@@ -500,16 +500,18 @@ __device__ __forceinline__ void frame_attn_exact_row(const vp2p_frame_attn_args&
   }
 }
 
-template <int D>
+template <int D, int KT>
 __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame_attn_args a) {
   using T = bf16;
   using M = Mfma<T>;
   using C = FrameCfg<T, D>;
   static_assert(C::ONES && D <= 64 && D % 8 == 0, "x2f: bf16, spare ones row");
-  constexpr int NBLK = C::KT / 32;
+  constexpr int NBLK = KT / 32;
+  constexpr int NCH = (KT * C::CPR + 255) / 256;          // 16-byte chunks per thread per tile
+  constexpr int LDS_BYTES = KT * (C::KROW + C::VROW) * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Ks = reinterpret_cast<T*>(smem);
-  T* Vs = Ks + C::KT * C::KROW;
+  T* Vs = Ks + KT * C::KROW;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int FQ = a.frames * a.tokens_q;
   const int qblocks = (FQ + 255) >> 8;
@@ -532,20 +534,20 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) qf[st][s] = qv[st] ? M::row_frag(qrow, s, h, D) : M::zero();
   }
-  for (int i = tid; i < C::LDS_BYTES / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0, 0, 0, 0};
+  for (int i = tid; i < LDS_BYTES / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0, 0, 0, 0};
   __syncthreads();
-  for (int k = tid; k < C::KT; k += 256) Vs[k * C::VROW + D] = (T)1.0f;   // O^T row D = sum_k p
+  for (int k = tid; k < KT; k += 256) Vs[k * C::VROW + D] = (T)1.0f;   // O^T row D = sum_k p
 
   const T* kbase = static_cast<const T*>(a.k) + b * a.k_sb + head * D;
   const T* vbase = static_cast<const T*>(a.v) + b * a.v_sb + head * D;
-  u32x4 kreg[C::NCH], vreg[C::NCH];
+  u32x4 kreg[NCH], vreg[NCH];
   auto load_tile = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < C::NCH; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * 256;
       const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
       const int key = kt + row;
-      if (c < C::KT * C::CPR && key < Nk) {
+      if (c < KT * C::CPR && key < Nk) {
         kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)key * a.k_sn + col);
         vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (int64_t)key * a.v_sn + col);
       } else {
@@ -556,9 +558,9 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   };
   auto store_tile = [&]() {
 #pragma unroll
-    for (int i = 0; i < C::NCH; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * 256;
-      if (c < C::KT * C::CPR) {
+      if (c < KT * C::CPR) {
         const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
         *reinterpret_cast<u32x4*>(Ks + row * C::KROW + col) = kreg[i];
         *reinterpret_cast<u32x4*>(Vs + row * C::VROW + col) = vreg[i];
@@ -649,11 +651,11 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
 
   load_tile(0);
   int kt = 0;
-  for (; kt + C::KT <= Nk; kt += C::KT) {
+  for (; kt + KT <= Nk; kt += KT) {
     __syncthreads();
     store_tile();
     __syncthreads();
-    if (kt + C::KT < Nk) load_tile(kt + C::KT);
+    if (kt + KT < Nk) load_tile(kt + KT);
     if (kt == 0) init_max();
     compute_tile(kt, std::false_type{});
   }
@@ -692,9 +694,9 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   }
 }
 
-static int k1_variant() {  // VP2P_K1_VARIANT=0 / 2 / 4 force the one-set / x2 / x2f kernels (A/B experiments)
+static int k1_variant() {  // VP2P_K1_VARIANT=0 / 2 / 4 / 5: one-set / x2 / x2f 128-key / x2f 256-key tiles (A/B)
   const char* e = getenv("VP2P_K1_VARIANT");
-  return e ? atoi(e) : 4;
+  return e ? atoi(e) : 5;
 }
 
 template <typename T, int D>
@@ -705,7 +707,15 @@ static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
     if (k1_variant() >= 4) {
       const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
       if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-      hipLaunchKernelGGL((frame_attn_kernel_x2f<D>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);
+      if (k1_variant() == 4) {
+        hipLaunchKernelGGL((frame_attn_kernel_x2f<D, 128>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);
+      } else {
+        constexpr int lds = 256 * (C::KROW + C::VROW) * 2;
+        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_x2f<D, 256>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+        if (!attr) return VP2P_E_LAUNCH;
+        hipLaunchKernelGGL((frame_attn_kernel_x2f<D, 256>), dim3((unsigned)nwg), dim3(256), lds, stream, *a);
+      }
       return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
     }
   }
