@@ -27,6 +27,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "video-p2p_amd"))
 
+# tuned MIOpen convolution database (tools/miopen_tune.py), unless the caller chose one
+if os.path.isdir(os.path.join(ROOT, "miopen_db")):
+    os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(ROOT, "miopen_db"))
+
 import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
@@ -48,8 +52,10 @@ def parse():
     ap.add_argument("--mode", default="edit", choices=["edit", "nulltext"],
                     help="edit: the P2P edit (BASELINE metric, configs[1]); nulltext: official-mode inversion "
                          "(DDIM inversion + null-text optimisation, configs[3]), one step = one inversion")
-    ap.add_argument("--conv-find", type=int, default=1,
-                    help="1 (default): let MIOpen benchmark its convolution solvers once per shape during warmup (torch.backends.cudnn.benchmark); 0: immediate-mode heuristics")
+    ap.add_argument("--conv-find", type=int, default=0,
+                    help="1: run MIOpen's solver search per new conv shape (torch.backends.cudnn.benchmark; slow "
+                         "warmup); 0 (default): immediate mode, which takes the tuned solvers recorded in the "
+                         "in-tree database miopen_db/ (tools/miopen_tune.py)")
     ap.add_argument("--inner-steps", type=int, default=10, help="null-text Adam iterations per DDIM step")
     ap.add_argument("--shard", default="clips", choices=["clips", "frames"],
                     help="clips: every rank edits its own clip (weak scaling, no collective); "
@@ -99,7 +105,7 @@ class K1Timer:
         return {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": src, "algorithmic_bytes": alg_bytes,
-                "kernel": "vp2p::frame_attn_kernel_x2<40> (res-64 FrameAttention, bf16)",
+                "kernel": "vp2p::frame_attn_kernel_x2f<40,256> (res-64 FrameAttention, bf16)",
                 "launches": len(ms), "avg_ms": round(sum(ms) / len(ms), 4),
                 "flops_per_launch": flops}
 
