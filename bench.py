@@ -27,10 +27,6 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "video-p2p_amd"))
 
-# tuned MIOpen convolution database (tools/miopen_tune.py), unless the caller chose one
-if os.path.isdir(os.path.join(ROOT, "miopen_db")):
-    os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(ROOT, "miopen_db"))
-
 import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
@@ -56,6 +52,8 @@ def parse():
                     help="1: run MIOpen's solver search per new conv shape (torch.backends.cudnn.benchmark; slow "
                          "warmup); 0 (default): immediate mode, which takes the tuned solvers recorded in the "
                          "in-tree database miopen_db/ (tools/miopen_tune.py)")
+    ap.add_argument("--tuned", type=int, default=1,
+                    help="1 (default): in-tree tuned MIOpen database (vp2p.tuning); 0: library heuristics")
     ap.add_argument("--inner-steps", type=int, default=10, help="null-text Adam iterations per DDIM step")
     ap.add_argument("--shard", default="clips", choices=["clips", "frames"],
                     help="clips: every rank edits its own clip (weak scaling, no collective); "
@@ -239,6 +237,9 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     torch.backends.cudnn.benchmark = bool(args.conv_find)
+    if args.tuned:
+        from vp2p.tuning import use_tuned_libraries
+        use_tuned_libraries()
     if args.mode == "nulltext":
         nulltext_main(args, world, rank, dev)
         if world > 1:

@@ -19,21 +19,17 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from vp2p.unet3d import UNet3DConditionModel, init_random_  # noqa: E402
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=8)
-    ap.add_argument("--batches", default="4,1,2")
-    ap.add_argument("--backward", default="1,2", help="batches also run through backward (null-text)")
-    args = ap.parse_args()
-    torch.backends.cudnn.benchmark = True
+def drive(frames, batches, backward):
+    """One UNet forward (and backward w.r.t. the embedding for the batches in ``backward``) at every
+    batch in ``batches``: every conv and GEMM shape the pipeline runs at ``frames`` frames, 512^2."""
     dev = torch.device("cuda")
     unet = init_random_(UNet3DConditionModel(), seed=0).to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
     unet.eval()
     unet.requires_grad_(False)   # null-text differentiates w.r.t. the embedding only
-    bwd = {int(b) for b in args.backward.split(",") if b}
-    for B in [int(b) for b in args.batches.split(",")]:
+    bwd = {int(b) for b in backward.split(",") if b}
+    for B in [int(b) for b in batches.split(",")]:
         t0 = time.time()
-        x = torch.randn(B, 4, args.frames, 64, 64, device=dev)
+        x = torch.randn(B, 4, frames, 64, 64, device=dev)
         ctx = torch.randn(B, 77, 768, device=dev, requires_grad=B in bwd)
         with torch.set_grad_enabled(B in bwd):
             out = unet(x, 981, ctx).sample
@@ -41,6 +37,16 @@ def main():
                 out.float().square().mean().backward()
         torch.cuda.synchronize()
         print(f"batch {B}{' +bwd' if B in bwd else ''}: {time.time() - t0:.1f} s", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--batches", default="4,1,2")
+    ap.add_argument("--backward", default="1,2", help="batches also run through backward (null-text)")
+    args = ap.parse_args()
+    torch.backends.cudnn.benchmark = True
+    drive(args.frames, args.batches, args.backward)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,27 @@
+"""Library-kernel selection recorded offline for the MI355X (no tuning at run time).
+
+Convolutions run on MIOpen.  ``miopen_db/`` holds MIOpen's user find/perf database for every
+convolution shape the pipeline runs, tuned on the MI355X by tools/miopen_tune.py
+(MIOPEN_FIND_ENFORCE=3: each solver's kernel parameters searched, the fastest recorded).  MIOpen
+reads ``MIOPEN_USER_DB_PATH`` when it initialises, so ``use_tuned_libraries()`` must run before the
+first convolution; immediate mode then takes the recorded solver of every shape instead of its
+heuristic, with no search at run time.
+
+(PyTorch TunableOp was tried for the GEMMs and rejected: its cold-cache timings picked solutions
+slower than hipBLASLt's own heuristic in the warm pipeline, 2.53 vs 2.46 s per edit.)
+"""
+from __future__ import annotations
+
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+MIOPEN_DB = os.path.join(ROOT, "miopen_db")
+
+
+def use_tuned_libraries() -> dict:
+    """Point MIOpen at the in-tree database (unless the caller chose one)."""
+    used = {}
+    if os.path.isdir(MIOPEN_DB):
+        os.environ.setdefault("MIOPEN_USER_DB_PATH", MIOPEN_DB)
+        used["miopen_db"] = os.environ["MIOPEN_USER_DB_PATH"]
+    return used
