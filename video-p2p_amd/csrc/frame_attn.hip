@@ -592,38 +592,38 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
 
   auto compute_tile = [&](int kt, auto masked_tag) {
     constexpr bool MASKED = decltype(masked_tag)::value;
+    auto qk = [&](int key0, int st) {
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int si = 0; si < C::KS; ++si)
+        acc = M::mma(*reinterpret_cast<const bf16x8*>(Ks + (key0 + r) * C::KROW + 16 * si + 8 * h), qf[st][si], acc);
+      if constexpr (MASKED) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (kt + key0 + acc_row(i, h) >= Nk) acc[i] = kNegInf;
+      }
+      return acc;
+    };
+    auto softmax_pv = [&](f32x16& sc, int key0, int st) {
+      const float nm = -m[st];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[i] = fast_exp2(__builtin_fmaf(sc[i], cs, nm));
+      const bf16x8 p0 = M::p_frag(sc, 0), p1 = M::p_frag(sc, 1);
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t) o[st][t] = M::mma(vt_frag_lds<C::VROW>(Vs, key0, 0, t), p0, o[st][t]);
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t) o[st][t] = M::mma(vt_frag_lds<C::VROW>(Vs, key0, 1, t), p1, o[st][t]);
+    };
+    // set 0's QK^T, then set 1's, so set 0's softmax runs while set 1's MFMAs execute and set 1's
+    // softmax while set 0's PV MFMAs execute (the other wave of the SIMD fills the rest)
 #pragma unroll
     for (int j = 0; j < NBLK; ++j) {
       const int key0 = 32 * j;
       if (MASKED && kt + key0 >= Nk) break;
-      // set 0's QK^T, then set 1's: set 0's softmax runs while set 1's MFMAs execute, and set 1's
-      // softmax while set 0's PV MFMAs execute
-      f32x16 s[2];
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        s[st] = zero16();
-#pragma unroll
-        for (int si = 0; si < C::KS; ++si) {
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ks + (key0 + r) * C::KROW + 16 * si + 8 * h);
-          s[st] = M::mma(af, qf[st][si], s[st]);
-        }
-      }
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        if constexpr (MASKED) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i)
-            if (kt + key0 + acc_row(i, h) >= Nk) s[st][i] = kNegInf;
-        }
-        const float nm = -m[st];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[st][i] = fast_exp2(__builtin_fmaf(s[st][i], cs, nm));
-        const bf16x8 p0 = M::p_frag(s[st], 0), p1 = M::p_frag(s[st], 1);
-#pragma unroll
-        for (int t = 0; t < C::NT; ++t) o[st][t] = M::mma(vt_frag_lds<C::VROW>(Vs, key0, 0, t), p0, o[st][t]);
-#pragma unroll
-        for (int t = 0; t < C::NT; ++t) o[st][t] = M::mma(vt_frag_lds<C::VROW>(Vs, key0, 1, t), p1, o[st][t]);
-      }
+      f32x16 s0 = qk(key0, 0);
+      f32x16 s1 = qk(key0, 1);
+      softmax_pv(s0, key0, 0);
+      softmax_pv(s1, key0, 1);
     }
     // once per tile: the tile's row sum (valid on lanes h == ONE_H; the other half reads a zero row)
     float lc[2];
