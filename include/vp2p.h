@@ -23,6 +23,9 @@
  *   vp2p_step_fused           CFG + DDIM step + LocalBlend: pipeline_tuneavideo.py:409-424 ->
  *                              dependent_ddim.py:268-309 (eta = 0) -> run_videop2p.py:142-155;
  *                              also NullInversion.next_step/prev_step (run_videop2p.py:445-463)
+ *   vp2p_group_norm_* / vp2p_layer_norm_* / vp2p_geglu_*  (K7-K9, their backward K7b-K9b)
+ *                              resnet.py:142,158, attention.py:110,200-216, FeedForward GEGLU
+ *   vp2p_conv2d_fwd           (K10) InflatedConv3d / resnet convs, resnet.py:11-19, 111-205
  */
 #ifndef VP2P_H
 #define VP2P_H
@@ -277,6 +280,25 @@ int vp2p_layer_norm_bwd(const vp2p_layer_norm_args* args, const void* dy, void* 
 /* x: the forward input (rows, 2*inner); dy: (rows, inner); dx: (rows, 2*inner) */
 int vp2p_geglu_bwd(const void* x, const void* dy, void* dx, int64_t rows, int32_t inner, int32_t dtype,
                    void* stream);
+
+/* ---- K10: implicit-GEMM convolution, channels-last bf16 -----------------------------------------
+ * nn.Conv2d of InflatedConv3d (tuneavideo/models/resnet.py:11-19: conv1/conv2/conv_shortcut of
+ * ResnetBlock3D :111-205, Downsample3D/Upsample3D convs) with the bias and, optionally, the resnet's
+ * shortcut add 'input_tensor + hidden_states' (:196-205) fused:  y = conv(x, w) + bias (+ residual).
+ * x: (batch, in_h, in_w, cin) contiguous; w: (cout, kernel, kernel, cin) contiguous (the memory of a
+ * channels_last conv weight); bias: (cout) or NULL; residual, y: (batch, out_h, out_w, cout).
+ * Supported: bf16, kernel 1 or 3, pad = (kernel-1)/2, stride 1 or 2, cin % 64 == 0, cout % 160 == 0;
+ * vp2p_conv2d_supported() reports it without launching (1 = yes). */
+typedef struct vp2p_conv_args {
+  const void* x; const void* w; const void* bias; const void* residual; void* y;
+  int32_t batch, in_h, in_w, cin;
+  int32_t cout, out_h, out_w;
+  int32_t kernel, stride, pad;
+  int32_t dtype;
+} vp2p_conv_args;
+
+int vp2p_conv2d_supported(const vp2p_conv_args* args);
+int vp2p_conv2d_fwd(const vp2p_conv_args* args, void* stream);
 
 /* ---- introspection ---------------------------------------------------------------------------- */
 int vp2p_abi_version(void);

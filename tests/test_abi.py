@@ -58,7 +58,7 @@ def test_struct_layout_matches_header(tmp_path):
                "vp2p_group_norm_args": _lib.GroupNormArgs, "vp2p_layer_norm_args": _lib.LayerNormArgs,
                "vp2p_frame_attn_bwd_args": _lib.FrameAttnBwdArgs,
                "vp2p_temporal_attn_bwd_args": _lib.TemporalAttnBwdArgs,
-               "vp2p_nulltext_loss_args": _lib.NullTextLossArgs}
+               "vp2p_nulltext_loss_args": _lib.NullTextLossArgs, "vp2p_conv_args": _lib.ConvArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

@@ -1,0 +1,61 @@
+"""K10 implicit-GEMM convolution vs an fp32 reference of the same op (F.conv2d in fp32 on the
+bf16-rounded inputs, plus the residual), for the conv shapes of the SD-1.5 UNet3D at reduced
+spatial size.  Tolerance: bf16 output rounding, 1e-2 of max|ref| (fp32 accumulation inside)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _case(n, cin, h, w, cout, k, stride, residual, seed=0):
+    from vp2p import ops
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, cin, h, w, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(cout, cin, k, k, generator=g) * (1.0 / (cin * k * k) ** 0.5)).to(torch.bfloat16)
+    b = (torch.randn(cout, generator=g) * 0.1).to(torch.bfloat16)
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = wt.to(DEV).contiguous(memory_format=torch.channels_last)
+    bd = b.to(DEV)
+    pad = (k - 1) // 2
+    ref = F.conv2d(xd.float(), wd.float(), bd.float(), stride, pad)
+    res = None
+    if residual:
+        res = torch.randn(ref.shape, generator=g).to(torch.bfloat16).to(DEV).contiguous(memory_format=torch.channels_last)
+        ref = ref.to(torch.bfloat16).float() + res.float()      # the reference rounds conv, then adds
+    assert ops.conv2d_supported(xd, wd, stride, pad)
+    out = ops.conv2d(xd, wd, bd, stride, pad, residual=res)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape and out.is_contiguous(memory_format=torch.channels_last)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("n,cin,h,w,cout,k,stride", [
+    (2, 320, 16, 16, 320, 3, 1),      # res-64 resnet conv
+    (2, 640, 8, 8, 1280, 3, 1),
+    (1, 2560, 4, 4, 1280, 3, 1),      # up-block concat input
+    (2, 960, 8, 8, 320, 3, 1),
+    (3, 320, 7, 9, 640, 3, 1),        # ragged M (189 pixels), odd sizes
+    (2, 320, 16, 16, 320, 3, 2),      # Downsample3D
+    (2, 640, 9, 11, 640, 3, 2),       # odd input, stride 2
+    (2, 960, 8, 8, 320, 1, 1),        # conv_shortcut 1x1
+    (1, 2560, 8, 8, 1280, 1, 1),
+])
+def test_conv2d(n, cin, h, w, cout, k, stride):
+    _case(n, cin, h, w, cout, k, stride, residual=False)
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_conv2d_residual(k):
+    _case(2, 640, 8, 8, 640, k, 1, residual=True, seed=1)
+
+
+def test_conv2d_unsupported_raises():
+    from vp2p import ops, _lib
+    x = torch.randn(1, 4, 8, 8, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = torch.randn(320, 4, 3, 3, device=DEV, dtype=torch.bfloat16)
+    assert not ops.conv2d_supported(x, wt, 1, 1)
+    with pytest.raises(_lib.Vp2pError):
+        ops.conv2d(x, wt, None, 1, 1)

@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "video-p2p_amd"))
 from vp2p.tuning import use_tuned_libraries  # noqa: E402
 
 use_tuned_libraries()
+from vp2p import ops  # noqa: E402
 from vp2p.unet3d import UNet3DConditionModel, init_random_  # noqa: E402
 
 
@@ -39,7 +40,7 @@ def main():
              torch.randn(args.batch, 77, 768, device=dev))
     for h in hs:
         h.remove()
-    total_ms, total_fl = 0.0, 0.0
+    total_ms, total_fl, total_best = 0.0, 0.0, 0.0
     rows = []
     for (xs, co, k, st, pad), n in sorted(shapes.items(), key=lambda t: -t[1]):
         x = torch.randn(xs, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -55,13 +56,30 @@ def main():
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / 10
         fl = 2.0 * y.numel() * xs[1] * k * k
+        row = {"x": xs, "cout": co, "k": k, "stride": st, "calls": n, "ms": round(ms, 4),
+               "tflops": round(fl / ms / 1e9, 1)}
+        best = ms
+        if ops.conv2d_supported(x, w, st, pad):
+            y2 = ops.conv2d(x, w, b, st, pad)
+            err = (y2.float() - y.float()).abs().max().item() / max(y.float().abs().max().item(), 1e-6)
+            for _ in range(3):
+                ops.conv2d(x, w, b, st, pad)
+            s.record()
+            for _ in range(10):
+                ops.conv2d(x, w, b, st, pad)
+            e.record()
+            torch.cuda.synchronize()
+            ms2 = s.elapsed_time(e) / 10
+            row.update({"k10_ms": round(ms2, 4), "k10_tflops": round(fl / ms2 / 1e9, 1), "k10_rel_err": round(err, 5)})
+            best = min(ms, ms2)
         total_ms += ms * n
+        total_best += best * n
         total_fl += fl * n
-        rows.append({"x": xs, "cout": co, "k": k, "stride": st, "calls": n, "ms": round(ms, 4),
-                     "tflops": round(fl / ms / 1e9, 1)})
+        rows.append(row)
         print(json.dumps(rows[-1]), flush=True)
     print(json.dumps({"total_ms_per_forward": round(total_ms, 3), "total_tflop": round(total_fl / 1e12, 3),
-                      "avg_tflops": round(total_fl / total_ms / 1e9, 1)}))
+                      "avg_tflops": round(total_fl / total_ms / 1e9, 1),
+                      "best_of_both_ms_per_forward": round(total_best, 3)}))
 
 
 if __name__ == "__main__":

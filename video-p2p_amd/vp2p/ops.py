@@ -449,3 +449,98 @@ def geglu_bwd(h: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
     check(_lib.load().vp2p_geglu_bwd(_ptr(h), _ptr(dy), _ptr(dh), h.numel() // (2 * inner), inner, dt, _stream()),
           "vp2p_geglu_bwd")
     return dh
+
+
+def _conv_args(x: torch.Tensor, weight: torch.Tensor, bias, residual, y, stride: int, padding: int):
+    N, Cin, H, W = x.shape
+    Cout, _, KH, KW = weight.shape
+    Ho = (H + 2 * padding - KH) // stride + 1
+    Wo = (W + 2 * padding - KW) // stride + 1
+    dt = _lib.BF16 if x.dtype == torch.bfloat16 else -1
+    return _lib.ConvArgs(_ptr(x), _ptr(weight), _ptr(bias), _ptr(residual), _ptr(y), N, H, W, Cin, Cout, Ho, Wo,
+                         KH if KH == KW else -1, stride, padding, dt), (N, Cout, Ho, Wo)
+
+
+def conv2d_supported(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0) -> bool:
+    """True when K10 covers this convolution: bf16, channels-last, 1x1 / 3x3 'same' padding, stride
+    1 or 2, Cin % 64 == 0, Cout % 160 == 0 (every resnet / up/down-sample conv of the SD-1.5 UNet
+    except conv_in / conv_out)."""
+    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4:
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    a, _ = _conv_args(x, weight, None, None, None, stride, padding)
+    return bool(_lib.load().vp2p_conv2d_supported(ctypes.byref(a)))
+
+
+def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
+           padding: int = 0, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K10: nn.Conv2d on channels-last bf16 with the bias and an optional residual add fused
+    (``residual + conv(x)``, the resnet shortcut add of resnet.py:196-205).  Returns a channels-last
+    (N, Cout, Ho, Wo) tensor.  Raises for shapes K10 does not cover (see ``conv2d_supported``)."""
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv2d: x must be channels-last contiguous")
+    w = weight if weight.is_contiguous(memory_format=torch.channels_last) else \
+        weight.contiguous(memory_format=torch.channels_last)
+    if bias is not None and (bias.dtype != x.dtype or not bias.is_contiguous()):
+        bias = bias.to(x.dtype).contiguous()
+    a, shape = _conv_args(x, w, bias, None, None, stride, padding)
+    y = torch.empty(shape, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    if residual is not None:
+        if residual.shape != y.shape or residual.dtype != y.dtype:
+            raise ValueError("conv2d: residual must match the output")
+        if not residual.is_contiguous(memory_format=torch.channels_last):
+            residual = residual.contiguous(memory_format=torch.channels_last)
+        a.residual = _ptr(residual)
+    a.y = _ptr(y)
+    check(_lib.load().vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd")
+    return y
+
+
+class ConvSelector:
+    """Per-shape choice between K10 and the library convolution (MIOpen), measured on the device
+    the first time a shape is seen (a few launches of each, timed with HIP events; the one sync
+    happens at that first call only, i.e. during warmup) and cached for the process."""
+
+    def __init__(self):
+        self.choice = {}
+        # VP2P_CONV=library | k10 | auto (default): A/B switch for experiments
+        import os
+        self.mode = os.environ.get("VP2P_CONV", "auto")
+
+    def run(self, x, weight, bias, stride: int, padding: int, residual, library):
+        key = (tuple(x.shape), tuple(weight.shape), stride, padding, residual is not None, x.device.index)
+        use = self.choice.get(key)
+        if use is None:
+            ok = self.mode != "library" and conv2d_supported(x, weight, stride, padding)
+            use = ok and (self.mode == "k10" or self._measure(x, weight, bias, stride, padding, residual, library))
+            self.choice[key] = use
+        if use:
+            return conv2d(x, weight, bias, stride, padding, residual=residual)
+        y = library()
+        return y if residual is None else residual + y
+
+    @staticmethod
+    def _measure(x, weight, bias, stride, padding, residual, library) -> bool:
+        def k10():
+            return conv2d(x, weight, bias, stride, padding, residual=residual)
+
+        def lib():
+            y = library()
+            return y if residual is None else residual + y
+
+        times = []
+        for fn in (k10, lib):
+            for _ in range(2):
+                fn()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(5):
+                fn()
+            e.record()
+            e.synchronize()
+            times.append(s.elapsed_time(e))
+        return times[0] < times[1]
+
+
+CONV = ConvSelector()

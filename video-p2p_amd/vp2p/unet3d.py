@@ -93,7 +93,19 @@ class TimestepEmbedding(nn.Module):
 
 
 class InflatedConv3d(nn.Conv2d):
-    """Per-frame Conv2d; input/output already '(b f) c h w'."""
+    """Per-frame Conv2d (resnet.py:11-19); input/output already '(b f) c h w' channels-last.
+
+    Runs on K10 (``ops.conv2d``, implicit GEMM with the bias and an optional residual add fused) or
+    on MIOpen, whichever ``ops.ConvSelector`` measured faster for this shape on this GPU; the choice
+    is made once per shape (first call) and cached.  ``residual``: added to the output (the resnet
+    shortcut add, fused on K10)."""
+
+    def forward(self, x, residual: Optional[torch.Tensor] = None):
+        if autograd.needs_grad(x, self.weight):
+            y = super().forward(x)
+            return y if residual is None else residual + y
+        return ops.CONV.run(x, self.weight, self.bias, self.stride[0], self.padding[0], residual,
+                            lambda: super(InflatedConv3d, self).forward(x))
 
 
 class ResnetBlock3D(nn.Module):
@@ -113,12 +125,11 @@ class ResnetBlock3D(nn.Module):
     def forward(self, x, temb, frames):
         h = self.conv1(group_norm_frames(x, self.norm1, frames, silu=True))
         t = self.time_emb_proj(F.silu(temb)).repeat_interleave(frames, 0).to(h.dtype)
-        h = self.conv2(self.dropout(group_norm_frames(h, self.norm2, frames, silu=True, add=t)))
         sc = x if self.conv_shortcut is None else self.conv_shortcut(x)
-        out = sc + h
+        h = self.dropout(group_norm_frames(h, self.norm2, frames, silu=True, add=t))
         if self.output_scale_factor != 1.0:
-            out = out / self.output_scale_factor
-        return out
+            return (sc + self.conv2(h)) / self.output_scale_factor
+        return self.conv2(h, residual=sc)          # sc + conv2(h): the add fused into K10's epilogue
 
 
 class GEGLU(nn.Module):
