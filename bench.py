@@ -45,9 +45,12 @@ def parse():
     ap.add_argument("--ddim-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-k1-events", action="store_true")
-    ap.add_argument("--mode", default="edit", choices=["edit", "nulltext"],
+    ap.add_argument("--mode", default="edit", choices=["edit", "nulltext", "k1long"],
                     help="edit: the P2P edit (BASELINE metric, configs[1]); nulltext: official-mode inversion "
-                         "(DDIM inversion + null-text optimisation, configs[3]), one step = one inversion")
+                         "(DDIM inversion + null-text optimisation, configs[3]), one step = one inversion; "
+                         "k1long: configs[4], the FrameAttention of one UNet forward over a --long-frames clip "
+                         "at 768^2, frames sharded over the ranks with the RCCL frame-0 K/V broadcast")
+    ap.add_argument("--long-frames", type=int, default=128, help="k1long: frames of the clip")
     ap.add_argument("--conv-find", type=int, default=0,
                     help="1: run MIOpen's solver search per new conv shape (torch.backends.cudnn.benchmark; slow "
                          "warmup); 0 (default): immediate mode, which takes the tuned solvers recorded in the "
@@ -174,6 +177,68 @@ def _cpu_model():
     return "unknown"
 
 
+def k1long_main(args, world, rank, dev):
+    """configs[4] of BASELINE.json: sparse-causal (first-frame K/V) attention of a 128-frame 768^2
+    clip, sharded by frames over the ranks.  One step = every attn1 call of one UNet forward at
+    UNet batch 4 (5 blocks at 96^2 tokens / C 320, 5 at 48^2 / 640, 5 at 24^2 / 1280, 1 at 12^2 / 1280):
+    per call rank 0 (owner of frame 0) broadcasts the frame-0 K/V (B, HW, 2C) over RCCL, then every
+    rank runs K1 on its f/G frames.  Synthetic bf16 activations; the projections are not timed."""
+    import torch.distributed as dist
+    from vp2p import ops
+    B, heads, f = 4, 8, args.long_frames
+    if f % world:
+        raise SystemExit(f"--long-frames {f} does not split over {world} ranks")
+    fl = f // world
+    levels = [(96 * 96, 320, 5), (48 * 48, 640, 5), (24 * 24, 1280, 5), (12 * 12, 1280, 1)]
+    g = torch.Generator(device=dev).manual_seed(3 + rank)
+    bufs = []
+    for hw, C, n in levels:
+        q = torch.randn(B * fl, hw, C, device=dev, dtype=torch.bfloat16, generator=g)
+        kv = torch.randn(B, hw, 2 * C, device=dev, dtype=torch.bfloat16, generator=g)
+        bufs.append((q, kv, torch.empty_like(q), C, n))
+
+    def step():
+        for q, kv, out, C, n in bufs:
+            for _ in range(n):
+                if world > 1:
+                    dist.broadcast(kv, src=0)
+                ops.frame_attention(q, kv[..., :C], kv[..., C:], fl, heads, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    flops = sum(4.0 * B * f * hw * hw * C * n for hw, C, n in levels)
+    result = {
+        "metric": "sparse-causal attention TFLOP/s, 768^2 x 128-frame clip (K1 + RCCL frame-0 K/V broadcast)",
+        "value": round(flops * args.steps / elapsed / 1e12, 1), "unit": "TFLOP/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random bf16 q / frame-0 k,v)",
+        "config": {"workload": f"attn1 of one UNet forward, {f} frames 768^2, UNet batch {B}, frame-sharded x{world}",
+                   "frames": f, "resolution": 768, "unet_batch": B, "parallelism": f"frame-sharded x{world} (RCCL)"},
+        "frames_per_s": round(f * args.steps / elapsed, 2),
+        "roofline": {"bound": "mfma", "achieved": round(flops / world * args.steps / elapsed / 1e12, 1),
+                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(flops / world * args.steps / elapsed / 1e12 / PEAK_BF16_TFLOPS, 4),
+                     "note": "per-GPU K1 algorithmic FLOP rate including the broadcast time"},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def nulltext_main(args, world, rank, dev):
     """configs[3] of BASELINE.json: NullInversion.invert (run_videop2p.py:614-624) of an 8-frame 512^2
     clip: 50 DDIM-inversion steps, then per step one conditional forward, up to --inner-steps
@@ -240,8 +305,8 @@ def main():
     if args.tuned:
         from vp2p.tuning import use_tuned_libraries
         use_tuned_libraries()
-    if args.mode == "nulltext":
-        nulltext_main(args, world, rank, dev)
+    if args.mode in ("nulltext", "k1long"):
+        (nulltext_main if args.mode == "nulltext" else k1long_main)(args, world, rank, dev)
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
