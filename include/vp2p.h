@@ -259,6 +259,9 @@ typedef struct vp2p_layer_norm_args {
 } vp2p_layer_norm_args;
 
 int vp2p_layer_norm_fwd(const vp2p_layer_norm_args* args, void* stream);
+/* The transformer block's residual add fused in front of the next LayerNorm (attention.py:247-268):
+ * sum = round(x + residual) (dtype), y = LayerNorm(sum).  sum may alias x or residual. */
+int vp2p_add_layer_norm_fwd(const vp2p_layer_norm_args* args, const void* residual, void* sum, void* stream);
 
 /* ---- K9: GEGLU gate ------------------------------------------------------------------------------
  * diffusers 0.11.1 GEGLU.forward after its projection: y = a * gelu(g), (a, g) = proj(x).chunk(2)

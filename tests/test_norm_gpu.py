@@ -101,6 +101,26 @@ def test_layer_norm(dtype, rows, C):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,C", [(1000, 320), (37, 640), (5, 1280)])
+def test_add_layer_norm(dtype, rows, C):
+    """Residual add fused into LayerNorm: the sum is bit-equal to torch's dtype add, the
+    normalised output matches F.layer_norm of that sum."""
+    from vp2p import ops
+    h = _rand((rows, C), 10, dtype, 2.0, 1.0)
+    x = _rand((rows, C), 11, dtype, 2.0)
+    w = _rand((C,), 12, dtype, 0.2, 1.0)
+    b = _rand((C,), 13, dtype, 0.2)
+    s_ref = h + x                                     # torch: one rounding to the dtype
+    ref = F.layer_norm(s_ref.float(), (C,), w.float(), b.float(), 1e-5)
+    hd = h.cuda()
+    s, y = ops.add_layer_norm(hd, x.cuda(), w.cuda(), b.cuda(), 1e-5)
+    torch.cuda.synchronize()
+    assert s.data_ptr() == hd.data_ptr()
+    assert torch.equal(s.cpu(), s_ref)
+    assert _rel(y.float(), ref) < TOL[dtype] * (3 if dtype == torch.float32 else 1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,inner", [(1000, 1280), (33, 2560), (7, 5120)])
 def test_geglu(dtype, rows, inner):
     from vp2p import ops

@@ -303,8 +303,12 @@ __device__ __forceinline__ float wave_sum(float x) {
   return x;
 }
 
-template <typename T, int NV, int RPW>
-__global__ __launch_bounds__(256) void ln_kernel(const vp2p_layer_norm_args a) {
+// ADD: the block's residual add fused in front (BasicTransformerBlock, attention.py:247-268:
+// 'hidden_states = attn(norm(hidden_states)) + hidden_states'): x_new = x + res, rounded to T and
+// written to sum (as the reference stores the sum), then normalised.
+template <typename T, int NV, int RPW, bool ADD = false>
+__global__ __launch_bounds__(256) void ln_kernel(const vp2p_layer_norm_args a, const T* res = nullptr,
+                                                 T* sum = nullptr) {
   const int lane = lane_id();
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   if (row0 >= a.rows) return;
@@ -320,6 +324,13 @@ __global__ __launch_bounds__(256) void ln_kernel(const vp2p_layer_norm_args a) {
       const int vi = lane + 64 * i;
       if (vi < nvec) {
         V8<T>::load(x + vi * 8, v[rr][i]);
+        if constexpr (ADD) {
+          float rv[8];
+          V8<T>::load(res + row * C + vi * 8, rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[rr][i][j] = (float)(T)(v[rr][i][j] + rv[j]);
+          if (row0 + rr < a.rows) V8<T>::store(sum + row * C + vi * 8, v[rr][i]);
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[rr][i][j] = 0.f;
@@ -719,6 +730,32 @@ extern "C" int vp2p_group_norm_fwd(const vp2p_group_norm_args* a, void* stream) 
   int rc = vp2p_group_norm_stats(a, stream);
   if (rc != VP2P_OK) return rc;
   return vp2p_group_norm_apply(a, a->partials, 1, stream);
+}
+
+extern "C" int vp2p_add_layer_norm_fwd(const vp2p_layer_norm_args* a, const void* residual, void* sum,
+                                       void* stream) {
+  if (!a || !a->x || !a->y || !residual || !sum || a->rows < 0) return VP2P_E_ARG;
+  if (a->dtype != VP2P_F32 && a->dtype != VP2P_BF16) return VP2P_E_DTYPE;
+  if (a->channels <= 0 || a->channels % 8 || a->channels > 2048) return VP2P_E_SHAPE;
+  if (a->rows == 0) return VP2P_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nv = (a->channels / 8 + 63) / 64;
+  const int rpw = nv == 1 ? 4 : nv == 2 ? 2 : 1;
+  const dim3 grid((unsigned)((a->rows + 4 * rpw - 1) / (4 * rpw))), block(256);
+#define VP2P_ALN(T)                                                                                          \
+  {                                                                                                          \
+    const T* r = static_cast<const T*>(residual);                                                            \
+    T* o = static_cast<T*>(sum);                                                                             \
+    switch (nv) {                                                                                            \
+      case 1: hipLaunchKernelGGL((ln_kernel<T, 1, 4, true>), grid, block, 0, s, *a, r, o); break;            \
+      case 2: hipLaunchKernelGGL((ln_kernel<T, 2, 2, true>), grid, block, 0, s, *a, r, o); break;            \
+      case 3: hipLaunchKernelGGL((ln_kernel<T, 3, 1, true>), grid, block, 0, s, *a, r, o); break;            \
+      default: hipLaunchKernelGGL((ln_kernel<T, 4, 1, true>), grid, block, 0, s, *a, r, o); break;           \
+    }                                                                                                        \
+  }
+  if (a->dtype == VP2P_BF16) VP2P_ALN(bf16) else VP2P_ALN(float)
+#undef VP2P_ALN
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
 extern "C" int vp2p_layer_norm_fwd(const vp2p_layer_norm_args* a, void* stream) {

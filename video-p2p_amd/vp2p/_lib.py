@@ -26,7 +26,8 @@ EXPORTS = ("vp2p_frame_attn_fwd", "vp2p_cross_kv_workspace_bytes", "vp2p_cross_k
            "vp2p_layer_norm_fwd", "vp2p_geglu_fwd",
            "vp2p_frame_attn_bwd_workspace_bytes", "vp2p_frame_attn_bwd", "vp2p_temporal_attn_bwd",
            "vp2p_group_norm_bwd_reduce", "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd",
-           "vp2p_nulltext_loss", "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd")
+           "vp2p_nulltext_loss", "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
+           "vp2p_add_layer_norm_fwd")
 
 
 class GroupNormArgs(ctypes.Structure):
@@ -164,13 +165,15 @@ def load(path: str = None):
     lib.vp2p_nulltext_loss_partials.argtypes = []
     lib.vp2p_conv2d_supported.argtypes = [POINTER(ConvArgs)]
     lib.vp2p_conv2d_fwd.argtypes = [POINTER(ConvArgs), c_void_p]
+    lib.vp2p_add_layer_norm_fwd.argtypes = [POINTER(LayerNormArgs), c_void_p, c_void_p, c_void_p]
     for name in ("vp2p_frame_attn_fwd", "vp2p_cross_kv_prep", "vp2p_cross_attn_p2p_fwd",
                  "vp2p_temporal_attn_p2p_fwd", "vp2p_step_fused", "vp2p_abi_version",
                  "vp2p_supported_head_dims", "vp2p_group_norm_parts", "vp2p_group_norm_stats",
                  "vp2p_group_norm_apply", "vp2p_group_norm_fwd", "vp2p_layer_norm_fwd", "vp2p_geglu_fwd",
                  "vp2p_frame_attn_bwd", "vp2p_temporal_attn_bwd", "vp2p_group_norm_bwd_reduce",
                  "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd", "vp2p_nulltext_loss",
-                 "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd"):
+                 "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
+                 "vp2p_add_layer_norm_fwd"):
         getattr(lib, name).restype = c_int32
     if lib.vp2p_abi_version() != ABI_VERSION:
         raise Vp2pError(f"{p}: ABI version {lib.vp2p_abi_version()} != {ABI_VERSION}; rebuild")

@@ -414,6 +414,24 @@ def layer_norm(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Optional[t
     return out
 
 
+def add_layer_norm(h: torch.Tensor, x: torch.Tensor, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
+                   eps: float):
+    """The transformer block's residual add fused into the next LayerNorm (K8 + add):
+    returns (s, y) with s = h + x (rounded to the dtype, written over ``h``) and y = LayerNorm(s)."""
+    if not h.is_contiguous() or not x.is_contiguous() or h.shape != x.shape:
+        raise ValueError("add_layer_norm: h and x must be contiguous tensors of one shape")
+    dt = _dtype(h, x)
+    C = h.shape[-1]
+    for t in (weight, bias):
+        if t is not None and (t.dtype != h.dtype or not t.is_contiguous()):
+            raise ValueError("weight/bias must be contiguous tensors of the activation dtype")
+    y = torch.empty_like(h)
+    a = _lib.LayerNormArgs(_ptr(h), _ptr(y), _ptr(weight), _ptr(bias), h.numel() // C, C, float(eps), dt)
+    check(_lib.load().vp2p_add_layer_norm_fwd(ctypes.byref(a), _ptr(x), _ptr(h), _stream()),
+          "vp2p_add_layer_norm_fwd")
+    return h, y
+
+
 def geglu(h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """GEGLU gate a * gelu(g) of a (..., 2*inner) projection (diffusers 0.11.1 GEGLU.forward)."""
     if not h.is_contiguous():

@@ -18,6 +18,7 @@ There is no CPU or PyTorch-op path: the model runs on the GPU only.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -59,6 +60,17 @@ def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
     if autograd.needs_grad(x, norm.weight, norm.bias):
         return autograd.LayerNormFn.apply(x, norm.weight, norm.bias, norm.eps)
     return ops.layer_norm(x, norm.weight, norm.bias, norm.eps)
+
+
+_FUSE_ADD_LN = os.environ.get("VP2P_FUSE_ADD_LN", "1") != "0"     # A/B switch for experiments
+
+
+def _add_ln(h: torch.Tensor, x: torch.Tensor, norm: nn.LayerNorm):
+    """(h + x, LayerNorm(h + x)) in one K8 pass; h is overwritten with the sum."""
+    if not _FUSE_ADD_LN or not h.is_contiguous() or h.shape != x.shape or not x.is_contiguous():
+        s = h + x
+        return s, layer_norm(norm, s)
+    return ops.add_layer_norm(h, x, norm.weight, norm.bias, norm.eps)
 
 
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0) -> torch.Tensor:
@@ -171,11 +183,20 @@ class BasicTransformerBlock(nn.Module):
         self.norm_temp = nn.LayerNorm(dim)
 
     def forward(self, x, context, frames):
-        x = self.attn1(layer_norm(self.norm1, x), video_length=frames) + x
-        x = self.attn2(layer_norm(self.norm2, x), encoder_hidden_states=context, video_length=frames) + x
-        x = self.ff(layer_norm(self.norm3, x)) + x
-        x = self.attn_temp(layer_norm(self.norm_temp, x), video_length=frames, temporal_layout="bf") + x
-        return x
+        if autograd.needs_grad(x):
+            x = self.attn1(layer_norm(self.norm1, x), video_length=frames) + x
+            x = self.attn2(layer_norm(self.norm2, x), encoder_hidden_states=context, video_length=frames) + x
+            x = self.ff(layer_norm(self.norm3, x)) + x
+            x = self.attn_temp(layer_norm(self.norm_temp, x), video_length=frames, temporal_layout="bf") + x
+            return x
+        # inference: each residual add is fused into the next LayerNorm (K8 + add), same roundings
+        h = self.attn1(layer_norm(self.norm1, x), video_length=frames)
+        x, y = _add_ln(h, x, self.norm2)
+        h = self.attn2(y, encoder_hidden_states=context, video_length=frames)
+        x, y = _add_ln(h, x, self.norm3)
+        h = self.ff(y)
+        x, y = _add_ln(h, x, self.norm_temp)
+        return self.attn_temp(y, video_length=frames, temporal_layout="bf") + x
 
 
 class Transformer3DModel(nn.Module):
