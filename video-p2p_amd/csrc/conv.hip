@@ -180,6 +180,149 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_kernel(const v
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// conv_kernel_g: the same 128 x 160 tile, staged by LDS-DMA (global_load_lds_dwordx4) into two LDS
+// stages, one barrier per K-step (the DMA of step s+1 runs under the MFMAs of step s; no VGPRs
+// hold the tile in flight).  A DMA instruction writes 64 x 16 B lane-linearly = 8 rows of 128 B;
+// the XOR swizzle lives in the per-lane SOURCE address: LDS slot j of row r holds global chunk
+// j ^ ((r >> 1) & 7), which makes the 16 rows of a 16-lane ds_read_b128 hit 16 distinct 4-bank
+// groups.  Padding taps and rows past M read a 16-byte zero vector in global memory.
+// ------------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) unsigned int kZero16[4] = {0, 0, 0, 0};
+
+constexpr int GBM = 128;
+constexpr int G_STAGE = (GBM + BN) * BK * 2;                 // bytes per stage (A then B), unpadded rows
+constexpr int G_LDS = 2 * G_STAGE > GBM * CROW * 2 ? 2 * G_STAGE : GBM * CROW * 2;
+constexpr int G_ADMA = GBM / 8 / 4;                          // A DMA instructions per wave per step: 4
+constexpr int G_BDMA = BN / 8 / 4;                           // B: 5
+
+__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+template <int KS>
+__global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int M = a.batch * a.out_h * a.out_w;
+  const int ntn = a.cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid - mt * ntn;
+  const int m0 = mt * GBM, n0 = nt * BN;
+  const bf16* x = static_cast<const bf16*>(a.x);
+  const bf16* wt = static_cast<const bf16*>(a.w);
+  const int Kw = KS * KS * a.cin;
+  const bf16* zero = reinterpret_cast<const bf16*>(kZero16);
+
+  // this lane's rows: A instruction i of wave w covers rows 8*(w + 4i) .. +7, lane row l / 8
+  const int lr = l >> 3, lj = l & 7;
+  int a_n[G_ADMA], a_iy[G_ADMA], a_ix[G_ADMA], a_c[G_ADMA];
+  bool a_ok[G_ADMA];
+#pragma unroll
+  for (int i = 0; i < G_ADMA; ++i) {
+    const int r = 8 * (w + 4 * i) + lr;
+    const int p = m0 + r;
+    a_ok[i] = p < M;
+    const int pp = a_ok[i] ? p : 0;
+    const int n = pp / (a.out_h * a.out_w), rem = pp - n * a.out_h * a.out_w;
+    const int oy = rem / a.out_w, ox = rem - oy * a.out_w;
+    a_n[i] = n;
+    a_iy[i] = oy * a.stride - a.pad;
+    a_ix[i] = ox * a.stride - a.pad;
+    a_c[i] = swz(r, lj) * 8;                                  // source channel offset of this lane
+  }
+  int b_c[G_BDMA];
+#pragma unroll
+  for (int i = 0; i < G_BDMA; ++i) b_c[i] = swz(8 * (w + 4 * i) + lr, lj) * 8;
+
+  const int csteps = a.cin / BK;
+  const int nsteps = KS * KS * csteps;
+  auto dma = [&](int step, int stage) {
+    const int tap = step / csteps, c0 = (step - tap * csteps) * BK;
+    const int kh = tap / KS, kw = tap - kh * KS;
+    char* As = smem + stage * G_STAGE;
+    char* Bs = As + GBM * BK * 2;
+#pragma unroll
+    for (int i = 0; i < G_ADMA; ++i) {
+      const int iy = a_iy[i] + kh, ix = a_ix[i] + kw;
+      const bool ok = a_ok[i] && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
+      const bf16* src = ok ? x + (((int64_t)a_n[i] * a.in_h + iy) * a.in_w + ix) * a.cin + c0 + a_c[i] : zero;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + 8 * (w + 4 * i) * BK * 2),
+                                       16, 0, 0);
+    }
+    const int64_t kofs = (int64_t)tap * a.cin + c0;
+#pragma unroll
+    for (int i = 0; i < G_BDMA; ++i) {
+      const int row = 8 * (w + 4 * i) + lr;
+      const bf16* src = wt + (int64_t)(n0 + row) * Kw + kofs + b_c[i];
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + 8 * (w + 4 * i) * BK * 2),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4v acc[WTM][WTN];
+#pragma unroll
+  for (int i = 0; i < WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < WTN; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = l & 15, fq = l >> 4;           // fragment row / 16-byte chunk within the 32-wide k-step
+  dma(0, 0);
+  for (int step = 0; step < nsteps; ++step) {
+    __syncthreads();                              // vmcnt(0): step's DMA landed; step-1's reads done
+    if (step + 1 < nsteps) dma(step + 1, (step + 1) & 1);
+    const char* As = smem + (step & 1) * G_STAGE;
+    const char* Bs = As + GBM * BK * 2;
+#pragma unroll
+    for (int ks = 0; ks < BK / 8; ks += 4) {      // chunk index of the k-step (0 or 4)
+      bf16x8 af[WTM], bfr[WTN];
+#pragma unroll
+      for (int i = 0; i < WTM; ++i) {
+        const int r = wm * 64 + 16 * i + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * BK * 2 + swz(r, ks + fq) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < WTN; ++j) {
+        const int r = wn * 80 + 16 * j + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK * 2 + swz(r, ks + fq) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+  }
+
+  __syncthreads();
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+  const bf16* bias = static_cast<const bf16*>(a.bias);
+#pragma unroll
+  for (int j = 0; j < WTN; ++j) {
+    const int col = wn * 80 + 16 * j + fr;
+    const float bv = bias ? (float)bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < WTM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Cs[(wm * 64 + 16 * i + 4 * fq + e) * CROW + col] = (bf16)(acc[i][j][e] + bv);
+  }
+  __syncthreads();
+  const bf16* res = static_cast<const bf16*>(a.residual);
+  bf16* y = static_cast<bf16*>(a.y);
+  for (int c = tid; c < GBM * (BN / 8); c += 256) {
+    const int row = c / (BN / 8), ch = c - row * (BN / 8);
+    const int p = m0 + row;
+    if (p >= M) continue;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+    const int64_t o = (int64_t)p * a.cout + n0 + ch * 8;
+    if (res) {
+      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)rv[j]);
+    }
+    *reinterpret_cast<bf16x8*>(y + o) = v;
+  }
+}
+
 }  // namespace conv
 }  // namespace vp2p
 
@@ -206,8 +349,25 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   if (M * a->cout > ((int64_t)1 << 40)) return VP2P_E_SHAPE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const char* e = getenv("VP2P_CONV_BM");           // A/B experiments: 128 or 256
-  const int bm = e ? atoi(e) : 128;
+  // default: the LDS-DMA kernel (conv_kernel_g); VP2P_CONV_BM=128 / 256 selects the register-staged
+  // kernels (A/B experiments)
+  const char* e = getenv("VP2P_CONV_BM");
+  const int bm = e ? atoi(e) : 1;
+  if (bm == 1) {
+    const int64_t nwg = (M + conv::GBM - 1) / conv::GBM * (a->cout / conv::BN);
+    if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+    static const bool attr =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<3>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<1>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess;
+    if (!attr) return VP2P_E_LAUNCH;
+    if (a->kernel == 3)
+      hipLaunchKernelGGL((conv::conv_kernel_g<3>), dim3((unsigned)nwg), dim3(256), conv::G_LDS, s, *a);
+    else
+      hipLaunchKernelGGL((conv::conv_kernel_g<1>), dim3((unsigned)nwg), dim3(256), conv::G_LDS, s, *a);
+    return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+  }
   auto launch = [&](auto bm_tag) {
     constexpr int BM = decltype(bm_tag)::value;
     constexpr int lds = conv::Cfg<BM>::LDS_BYTES;
