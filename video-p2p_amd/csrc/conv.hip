@@ -190,16 +190,25 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_kernel(const v
 // ------------------------------------------------------------------------------------------------
 __device__ __attribute__((aligned(16))) unsigned int kZero16[4] = {0, 0, 0, 0};
 
-constexpr int GBM = 128;
-constexpr int G_STAGE = (GBM + BN) * BK * 2;                 // bytes per stage (A then B), unpadded rows
-constexpr int G_LDS = 2 * G_STAGE > GBM * CROW * 2 ? 2 * G_STAGE : GBM * CROW * 2;
-constexpr int G_ADMA = GBM / 8 / 4;                          // A DMA instructions per wave per step: 4
-constexpr int G_BDMA = BN / 8 / 4;                           // B: 5
+// GBM = 128 (4 waves, 2 workgroups per CU) or 256 (8 waves, one per CU); waves (GBM/64) x 2
+template <int GBM, int NS = 2>
+struct GCfg {
+  static constexpr int NW = GBM / 32;
+  static constexpr int STAGE = (GBM + BN) * BK * 2;              // bytes per stage (A then B)
+  static constexpr int LDS = NS * STAGE > GBM * CROW * 2 ? NS * STAGE : GBM * CROW * 2;
+  static constexpr int ADMA = GBM / 8 / NW;                      // A DMA instructions per wave per step: 4
+  static constexpr int BDMA = (BN / 8 + NW - 1) / NW;            // B: 5 (4 waves) or 3 (8 waves, last ragged)
+};
 
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
-template <int KS>
-__global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) {
+// NS = 2: one step in flight, __syncthreads per step.  NS = 3: two steps in flight; each wave
+// waits (counted vmcnt) only for its own DMA of the step it is about to read, then a raw
+// s_barrier -- the newer step's DMA stays in flight across it.
+template <int KS, int GBM, int NS>
+__global__ __launch_bounds__(GBM * 2, GBM == 128 && NS == 2 ? 2 : 1) void conv_kernel_g(const vp2p_conv_args a) {
+  using G = GCfg<GBM, NS>;
+  constexpr int NW = G::NW, G_STAGE = G::STAGE, G_ADMA = G::ADMA, G_BDMA = G::BDMA;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
@@ -219,7 +228,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
   bool a_ok[G_ADMA];
 #pragma unroll
   for (int i = 0; i < G_ADMA; ++i) {
-    const int r = 8 * (w + 4 * i) + lr;
+    const int r = 8 * (w + NW * i) + lr;
     const int p = m0 + r;
     a_ok[i] = p < M;
     const int pp = a_ok[i] ? p : 0;
@@ -232,7 +241,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
   }
   int b_c[G_BDMA];
 #pragma unroll
-  for (int i = 0; i < G_BDMA; ++i) b_c[i] = swz(8 * (w + 4 * i) + lr, lj) * 8;
+  for (int i = 0; i < G_BDMA; ++i) b_c[i] = swz(8 * (w + NW * i) + lr, lj) * 8;
 
   const int csteps = a.cin / BK;
   const int nsteps = KS * KS * csteps;
@@ -246,15 +255,16 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
       const int iy = a_iy[i] + kh, ix = a_ix[i] + kw;
       const bool ok = a_ok[i] && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
       const bf16* src = ok ? x + (((int64_t)a_n[i] * a.in_h + iy) * a.in_w + ix) * a.cin + c0 + a_c[i] : zero;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + 8 * (w + 4 * i) * BK * 2),
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
                                        16, 0, 0);
     }
     const int64_t kofs = (int64_t)tap * a.cin + c0;
 #pragma unroll
     for (int i = 0; i < G_BDMA; ++i) {
-      const int row = 8 * (w + 4 * i) + lr;
+      if (BN / 8 % NW && w + NW * i >= BN / 8) break;           // 8-wave tile: 20 row groups over 8 waves
+      const int row = 8 * (w + NW * i) + lr;
       const bf16* src = wt + (int64_t)(n0 + row) * Kw + kofs + b_c[i];
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + 8 * (w + 4 * i) * BK * 2),
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + 8 * (w + NW * i) * BK * 2),
                                        16, 0, 0);
     }
   };
@@ -266,11 +276,28 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
     for (int j = 0; j < WTN; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
   const int fr = l & 15, fq = l >> 4;           // fragment row / 16-byte chunk within the 32-wide k-step
+  // DMA instructions this wave issues per step (the last B row groups are ragged over 8 waves)
+  const int ndma = G_ADMA + ((BN / 8 % NW) ? (w < BN / 8 % NW ? G_BDMA : G_BDMA - 1) : G_BDMA);
   dma(0, 0);
+  if (NS == 3 && nsteps > 1) dma(1, 1);
   for (int step = 0; step < nsteps; ++step) {
-    __syncthreads();                              // vmcnt(0): step's DMA landed; step-1's reads done
-    if (step + 1 < nsteps) dma(step + 1, (step + 1) & 1);
-    const char* As = smem + (step & 1) * G_STAGE;
+    if constexpr (NS == 2) {
+      __syncthreads();                            // vmcnt(0): step's DMA landed; step-1's reads done
+      if (step + 1 < nsteps) dma(step + 1, (step + 1) & 1);
+    } else {
+      // own DMA of `step` landed (the newer step's may still fly), then everyone's
+      if (step + 1 < nsteps) {
+        if (ndma == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        else if (ndma == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (step + 2 < nsteps) dma(step + 2, (step + 2) % 3);
+    }
+    const char* As = smem + (NS == 2 ? (step & 1) : (step % 3)) * G_STAGE;
     const char* Bs = As + GBM * BK * 2;
 #pragma unroll
     for (int ks = 0; ks < BK / 8; ks += 4) {      // chunk index of the k-step (0 or 4)
@@ -308,7 +335,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
   __syncthreads();
   const bf16* res = static_cast<const bf16*>(a.residual);
   bf16* y = static_cast<bf16*>(a.y);
-  for (int c = tid; c < GBM * (BN / 8); c += 256) {
+  for (int c = tid; c < GBM * (BN / 8); c += GBM * 2) {
     const int row = c / (BN / 8), ch = c - row * (BN / 8);
     const int p = m0 + row;
     if (p >= M) continue;
@@ -349,24 +376,32 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   if (M * a->cout > ((int64_t)1 << 40)) return VP2P_E_SHAPE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // default: the LDS-DMA kernel (conv_kernel_g); VP2P_CONV_BM=128 / 256 selects the register-staged
-  // kernels (A/B experiments)
+  // default (1): the LDS-DMA kernel conv_kernel_g with 128-row tiles; 2: its 256-row (8-wave) form;
+  // 3: 256-row tiles with three LDS stages (two steps in flight);
+  // 128 / 256: the register-staged kernels (A/B experiments)
   const char* e = getenv("VP2P_CONV_BM");
   const int bm = e ? atoi(e) : 1;
-  if (bm == 1) {
-    const int64_t nwg = (M + conv::GBM - 1) / conv::GBM * (a->cout / conv::BN);
-    if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-    static const bool attr =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<3>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<1>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess;
-    if (!attr) return VP2P_E_LAUNCH;
-    if (a->kernel == 3)
-      hipLaunchKernelGGL((conv::conv_kernel_g<3>), dim3((unsigned)nwg), dim3(256), conv::G_LDS, s, *a);
-    else
-      hipLaunchKernelGGL((conv::conv_kernel_g<1>), dim3((unsigned)nwg), dim3(256), conv::G_LDS, s, *a);
-    return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+  if (bm >= 1 && bm <= 3) {
+    auto launch_g = [&](auto gbm_tag, auto ns_tag) {
+      constexpr int GBM = decltype(gbm_tag)::value, NS = decltype(ns_tag)::value;
+      constexpr int lds = conv::GCfg<GBM, NS>::LDS;
+      const int64_t nwg = (M + GBM - 1) / GBM * (a->cout / conv::BN);
+      if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+      static const bool attr =
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<3, GBM, NS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess &&
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<1, GBM, NS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+      if (!attr) return VP2P_E_LAUNCH;
+      if (a->kernel == 3)
+        hipLaunchKernelGGL((conv::conv_kernel_g<3, GBM, NS>), dim3((unsigned)nwg), dim3(2 * GBM), lds, s, *a);
+      else
+        hipLaunchKernelGGL((conv::conv_kernel_g<1, GBM, NS>), dim3((unsigned)nwg), dim3(2 * GBM), lds, s, *a);
+      return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+    };
+    if (bm == 3) return launch_g(std::integral_constant<int, 256>{}, std::integral_constant<int, 3>{});
+    if (bm == 2) return launch_g(std::integral_constant<int, 256>{}, std::integral_constant<int, 2>{});
+    return launch_g(std::integral_constant<int, 128>{}, std::integral_constant<int, 2>{});
   }
   auto launch = [&](auto bm_tag) {
     constexpr int BM = decltype(bm_tag)::value;
