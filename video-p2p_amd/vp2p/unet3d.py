@@ -113,7 +113,7 @@ class InflatedConv3d(nn.Conv2d):
     shortcut add, fused on K10)."""
 
     def forward(self, x, residual: Optional[torch.Tensor] = None):
-        if autograd.needs_grad(x, self.weight):
+        if autograd.needs_grad(x, self.weight, residual):
             y = super().forward(x)
             return y if residual is None else residual + y
         return ops.CONV.run(x, self.weight, self.bias, self.stride[0], self.padding[0], residual,
@@ -183,7 +183,7 @@ class BasicTransformerBlock(nn.Module):
         self.norm_temp = nn.LayerNorm(dim)
 
     def forward(self, x, context, frames):
-        if autograd.needs_grad(x):
+        if torch.is_grad_enabled():         # autograd may need any branch (e.g. only attn2 sees the embedding)
             x = self.attn1(layer_norm(self.norm1, x), video_length=frames) + x
             x = self.attn2(layer_norm(self.norm2, x), encoder_hidden_states=context, video_length=frames) + x
             x = self.ff(layer_norm(self.norm3, x)) + x
