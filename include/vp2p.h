@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 2
+#define VP2P_ABI_VERSION 3
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -292,12 +292,21 @@ int vp2p_geglu_bwd(const void* x, const void* dy, void* dx, int64_t rows, int32_
  * channels_last conv weight); bias: (cout) or NULL; residual, y: (batch, out_h, out_w, cout).
  * Supported: bf16, kernel 1 or 3, pad = (kernel-1)/2, stride 1 or 2, cin % 64 == 0, cout % 160 == 0;
  * vp2p_conv2d_supported() reports it without launching (1 = yes). */
+enum vp2p_conv_epilogue {
+  VP2P_CONV_EPI_NONE = 0,
+  /* diffusers GEGLU after its projection (FeedForward, attention.py:190,259): kernel 1, no residual;
+   * w/bias rows interleaved per 160-row tile as [80 value rows, the 80 matching gate rows]; y is
+   * (batch*in_h*in_w, cout/2) = value * gelu(gate), rounded like K9. */
+  VP2P_CONV_EPI_GEGLU = 1
+};
+
 typedef struct vp2p_conv_args {
   const void* x; const void* w; const void* bias; const void* residual; void* y;
   int32_t batch, in_h, in_w, cin;
   int32_t cout, out_h, out_w;
   int32_t kernel, stride, pad;
   int32_t dtype;
+  int32_t epilogue;         /* vp2p_conv_epilogue */
 } vp2p_conv_args;
 
 int vp2p_conv2d_supported(const vp2p_conv_args* args);

@@ -59,3 +59,24 @@ def test_conv2d_unsupported_raises():
     assert not ops.conv2d_supported(x, wt, 1, 1)
     with pytest.raises(_lib.Vp2pError):
         ops.conv2d(x, wt, None, 1, 1)
+
+
+@pytest.mark.parametrize("M,K,inner", [(1000, 320, 1280), (257, 640, 2560), (64, 1280, 5120)])
+def test_linear_geglu(M, K, inner):
+    """K10 with the GEGLU epilogue vs F.linear + diffusers GEGLU in fp32 on the same bf16 inputs
+    (projection rounded to bf16, gelu rounded, product rounded -- torch's eager roundings)."""
+    from vp2p import ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(2 * inner, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(2 * inner, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    h = F.linear(x.float(), w.float(), b.float()).to(torch.bfloat16).float()
+    a, gt = h.chunk(2, dim=-1)
+    ref = a * F.gelu(gt).to(torch.bfloat16).float()
+    assert ops.linear_geglu_supported(x, w)
+    wi, bi = ops.geglu_interleave(w, b)
+    out = ops.linear_geglu(x, wi, bi)
+    torch.cuda.synchronize()
+    assert out.shape == (M, inner)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err

@@ -205,7 +205,10 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 // NS = 2: one step in flight, __syncthreads per step.  NS = 3: two steps in flight; each wave
 // waits (counted vmcnt) only for its own DMA of the step it is about to read, then a raw
 // s_barrier -- the newer step's DMA stays in flight across it.
-template <int KS, int GBM, int NS>
+// EPI = 1 (GEGLU, 1x1 only): the weight rows come interleaved per 160-column tile as [80 "a" rows,
+// the 80 matching "gate" rows], and the epilogue writes y[p, nt*80 + j] = a * gelu(g) (exact erf,
+// each step rounded to bf16 as torch's eager GEGLU does) into a (M, cout/2) output.
+template <int KS, int GBM, int NS, int EPI = 0>
 __global__ __launch_bounds__(GBM * 2, GBM == 128 && NS == 2 ? 2 : 1) void conv_kernel_g(const vp2p_conv_args a) {
   using G = GCfg<GBM, NS>;
   constexpr int NW = G::NW, G_STAGE = G::STAGE, G_ADMA = G::ADMA, G_BDMA = G::BDMA;
@@ -335,6 +338,27 @@ __global__ __launch_bounds__(GBM * 2, GBM == 128 && NS == 2 ? 2 : 1) void conv_k
   __syncthreads();
   const bf16* res = static_cast<const bf16*>(a.residual);
   bf16* y = static_cast<bf16*>(a.y);
+  if constexpr (EPI == 1) {
+#pragma clang fp contract(off)
+    constexpr float kAlpha = 0.70710678118654752440f;
+    const int half = a.cout / 2;
+    for (int c = tid; c < GBM * (BN / 16); c += GBM * 2) {
+      const int row = c / (BN / 16), ch = c - row * (BN / 16);
+      const int p = m0 + row;
+      if (p >= M) continue;
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+      const bf16x8 gv = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + BN / 2 + ch * 8);
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = (float)gv[j];
+        const float ge = (float)(bf16)(g * 0.5f * (1.f + erff(g * kAlpha)));
+        v[j] = (bf16)((float)av[j] * ge);
+      }
+      *reinterpret_cast<bf16x8*>(y + (int64_t)p * half + nt * (BN / 2) + ch * 8) = v;
+    }
+    return;
+  }
   for (int c = tid; c < GBM * (BN / 8); c += GBM * 2) {
     const int row = c / (BN / 8), ch = c - row * (BN / 8);
     const int p = m0 + row;
@@ -364,6 +388,8 @@ extern "C" int vp2p_conv2d_supported(const vp2p_conv_args* a) {
   if (a->batch <= 0 || a->in_h <= 0 || a->in_w <= 0) return 0;
   if (a->out_h != (a->in_h + 2 * a->pad - a->kernel) / a->stride + 1) return 0;
   if (a->out_w != (a->in_w + 2 * a->pad - a->kernel) / a->stride + 1) return 0;
+  if (a->epilogue != VP2P_CONV_EPI_NONE &&
+      (a->epilogue != VP2P_CONV_EPI_GEGLU || a->kernel != 1 || a->stride != 1 || a->residual)) return 0;
   return 1;
 }
 
@@ -381,6 +407,7 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   // 128 / 256: the register-staged kernels (A/B experiments)
   const char* e = getenv("VP2P_CONV_BM");
   const int bm = e ? atoi(e) : 1;
+  if (a->epilogue != VP2P_CONV_EPI_NONE && !(bm >= 1 && bm <= 3)) return VP2P_E_SHAPE;
   if (bm >= 1 && bm <= 3) {
     auto launch_g = [&](auto gbm_tag, auto ns_tag) {
       constexpr int GBM = decltype(gbm_tag)::value, NS = decltype(ns_tag)::value;
@@ -391,9 +418,13 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
           hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<3, GBM, NS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess &&
           hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<1, GBM, NS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess &&
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<1, GBM, NS, 1>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
       if (!attr) return VP2P_E_LAUNCH;
-      if (a->kernel == 3)
+      if (a->epilogue == VP2P_CONV_EPI_GEGLU)
+        hipLaunchKernelGGL((conv::conv_kernel_g<1, GBM, NS, 1>), dim3((unsigned)nwg), dim3(2 * GBM), lds, s, *a);
+      else if (a->kernel == 3)
         hipLaunchKernelGGL((conv::conv_kernel_g<3, GBM, NS>), dim3((unsigned)nwg), dim3(2 * GBM), lds, s, *a);
       else
         hipLaunchKernelGGL((conv::conv_kernel_g<1, GBM, NS>), dim3((unsigned)nwg), dim3(2 * GBM), lds, s, *a);

@@ -13,9 +13,10 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
+CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
 STATUS = {0: "OK", -1: "VP2P_E_ARG", -2: "VP2P_E_DTYPE", -3: "VP2P_E_HEAD_DIM", -4: "VP2P_E_SHAPE",
           -5: "VP2P_E_LAUNCH"}
 
@@ -41,7 +42,8 @@ class ConvArgs(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("residual", c_void_p), ("y", c_void_p),
                 ("batch", c_int32), ("in_h", c_int32), ("in_w", c_int32), ("cin", c_int32),
                 ("cout", c_int32), ("out_h", c_int32), ("out_w", c_int32),
-                ("kernel", c_int32), ("stride", c_int32), ("pad", c_int32), ("dtype", c_int32)]
+                ("kernel", c_int32), ("stride", c_int32), ("pad", c_int32), ("dtype", c_int32),
+                ("epilogue", c_int32)]
 
 
 class LayerNormArgs(ctypes.Structure):

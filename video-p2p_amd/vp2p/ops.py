@@ -516,9 +516,10 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
 
 
 class ConvSelector:
-    """Per-shape choice between K10 and the library convolution (MIOpen), measured on the device
-    the first time a shape is seen (a few launches of each, timed with HIP events; the one sync
-    happens at that first call only, i.e. during warmup) and cached for the process."""
+    """Per-shape choice between a K10 launch and the library path (MIOpen convolution, hipBLASLt
+    GEMM + K9), measured on the device the first time a shape is seen (a few launches of each,
+    timed with HIP events; the one sync happens at that first call only, i.e. during warmup) and
+    cached for the process."""
 
     def __init__(self):
         self.choice = {}
@@ -526,20 +527,15 @@ class ConvSelector:
         import os
         self.mode = os.environ.get("VP2P_CONV", "auto")
 
-    def run(self, x, weight, bias, stride: int, padding: int, residual, library):
-        key = (tuple(x.shape), tuple(weight.shape), stride, padding, residual is not None, x.device.index)
+    def pick(self, key, supported: bool, k10, library) -> bool:
         use = self.choice.get(key)
         if use is None:
-            ok = self.mode != "library" and conv2d_supported(x, weight, stride, padding)
-            use = ok and (self.mode == "k10" or self._measure(x, weight, bias, stride, padding, residual, library))
+            ok = self.mode != "library" and supported
+            use = ok and (self.mode == "k10" or self._faster(k10, library))
             self.choice[key] = use
-        if use:
-            return conv2d(x, weight, bias, stride, padding, residual=residual)
-        y = library()
-        return y if residual is None else residual + y
+        return use
 
-    @staticmethod
-    def _measure(x, weight, bias, stride, padding, residual, library) -> bool:
+    def run(self, x, weight, bias, stride: int, padding: int, residual, library):
         def k10():
             return conv2d(x, weight, bias, stride, padding, residual=residual)
 
@@ -547,8 +543,15 @@ class ConvSelector:
             y = library()
             return y if residual is None else residual + y
 
+        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, residual is not None, x.device.index)
+        if self.pick(key, conv2d_supported(x, weight, stride, padding), k10, lib):
+            return k10()
+        return lib()
+
+    @staticmethod
+    def _faster(k10, library) -> bool:
         times = []
-        for fn in (k10, lib):
+        for fn in (k10, library):
             for _ in range(2):
                 fn()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -562,3 +565,38 @@ class ConvSelector:
 
 
 CONV = ConvSelector()
+
+
+def geglu_interleave(weight: torch.Tensor, bias: Optional[torch.Tensor]):
+    """Row order K10's GEGLU epilogue expects: per 160-row tile, 80 value rows then the 80 matching
+    gate rows (GEGLU.proj is [value; gate], diffusers' ``chunk(2, dim=-1)``)."""
+    n2, k = weight.shape
+    inner = n2 // 2
+    if inner % 80:
+        raise ValueError("GEGLU inner width must be a multiple of 80")
+    t = inner // 80
+    w = torch.stack([weight[:inner].reshape(t, 80, k), weight[inner:].reshape(t, 80, k)], 1).reshape(n2, k)
+    b = None if bias is None else torch.stack([bias[:inner].reshape(t, 80), bias[inner:].reshape(t, 80)], 1).reshape(n2)
+    return w.contiguous(), (None if b is None else b.contiguous())
+
+
+def linear_geglu_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or not x.is_cuda or not x.is_contiguous():
+        return False
+    M = x.numel() // x.shape[-1]
+    a = _lib.ConvArgs(None, None, None, None, None, 1, M, 1, x.shape[-1], weight.shape[0], M, 1, 1, 1, 0,
+                      _lib.BF16, _lib.CONV_EPI_GEGLU)
+    return weight.shape[0] % 160 == 0 and bool(_lib.load().vp2p_conv2d_supported(ctypes.byref(a)))
+
+
+def linear_geglu(x: torch.Tensor, w_il: torch.Tensor, b_il: Optional[torch.Tensor]) -> torch.Tensor:
+    """GEGLU(x) = value * gelu(gate) with (value, gate) = x @ W^T + b, in one K10 launch (the
+    projection's (M, 2*inner) output is never written).  ``w_il``/``b_il`` from ``geglu_interleave``."""
+    K = x.shape[-1]
+    M = x.numel() // K
+    n2 = w_il.shape[0]
+    y = torch.empty(*x.shape[:-1], n2 // 2, device=x.device, dtype=x.dtype)
+    a = _lib.ConvArgs(_ptr(x), _ptr(w_il), _ptr(b_il), None, _ptr(y), 1, M, 1, K, n2, M, 1, 1, 1, 0,
+                      _lib.BF16, _lib.CONV_EPI_GEGLU)
+    check(_lib.load().vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd(geglu)")
+    return y

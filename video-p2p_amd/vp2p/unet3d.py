@@ -62,7 +62,8 @@ def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
     return ops.layer_norm(x, norm.weight, norm.bias, norm.eps)
 
 
-_FUSE_ADD_LN = os.environ.get("VP2P_FUSE_ADD_LN", "1") != "0"     # A/B switch for experiments
+_FUSE_ADD_LN = os.environ.get("VP2P_FUSE_ADD_LN", "1") != "0"     # A/B switches for experiments
+_FUSE_GEGLU = os.environ.get("VP2P_FUSE_GEGLU", "1") != "0"
 
 
 def _add_ln(h: torch.Tensor, x: torch.Tensor, norm: nn.LayerNorm):
@@ -150,10 +151,29 @@ class GEGLU(nn.Module):
         self.proj = nn.Linear(dim_in, dim_out * 2)
 
     def forward(self, x):
-        h = self.proj(x)
-        if autograd.needs_grad(h):
-            return autograd.GEGLUFn.apply(h)
-        return ops.geglu(h)
+        if autograd.needs_grad(x, self.proj.weight):
+            return autograd.GEGLUFn.apply(self.proj(x))
+
+        def unfused():
+            return ops.geglu(self.proj(x))
+
+        def fused():       # projection + GEGLU in one K10 launch: the (rows, 2*inner) tensor is never stored
+            return ops.linear_geglu(x, *self._interleaved())
+
+        # measured per shape: K10 wins where K is small (res-64, K = 320), hipBLASLt's GEMM elsewhere
+        key = ("geglu", tuple(x.shape), tuple(self.proj.weight.shape), x.device.index)
+        ok = _FUSE_GEGLU and ops.linear_geglu_supported(x, self.proj.weight)
+        return fused() if ops.CONV.pick(key, ok, fused, unfused) else unfused()
+
+    def _interleaved(self):
+        w, b = self.proj.weight, self.proj.bias
+        key = (w.data_ptr(), w._version, None if b is None else (b.data_ptr(), b._version))
+        hit = getattr(self, "_il", None)
+        if hit is None or hit[0] != key:
+            with torch.no_grad():
+                hit = (key, ops.geglu_interleave(w.detach(), None if b is None else b.detach()))
+            object.__setattr__(self, "_il", hit)
+        return hit[1]
 
 
 class FeedForward(nn.Module):
