@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 3
+#define VP2P_ABI_VERSION 4
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -307,9 +307,13 @@ typedef struct vp2p_conv_args {
   int32_t kernel, stride, pad;
   int32_t dtype;
   int32_t epilogue;         /* vp2p_conv_epilogue */
+  float* workspace;         /* fp32 split-K slices, vp2p_conv2d_workspace_bytes() bytes, or NULL (one pass) */
+  int32_t ksplit;           /* set by the library; callers leave 0 */
 } vp2p_conv_args;
 
 int vp2p_conv2d_supported(const vp2p_conv_args* args);
+/* Workspace the shape wants for split-K (small-M shapes: fewer tiles than CUs); 0 = none. */
+int64_t vp2p_conv2d_workspace_bytes(const vp2p_conv_args* args);
 int vp2p_conv2d_fwd(const vp2p_conv_args* args, void* stream);
 
 /* ---- introspection ---------------------------------------------------------------------------- */

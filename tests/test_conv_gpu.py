@@ -42,6 +42,8 @@ def _case(n, cin, h, w, cout, k, stride, residual, seed=0):
     (2, 640, 9, 11, 640, 3, 2),       # odd input, stride 2
     (2, 960, 8, 8, 320, 1, 1),        # conv_shortcut 1x1
     (1, 2560, 8, 8, 1280, 1, 1),
+    (32, 1280, 8, 8, 1280, 3, 1),     # res-8: 128 tiles -> split-K with fp32 workspace
+    (32, 2560, 8, 8, 1280, 1, 1),     # split-K, 1x1
 ])
 def test_conv2d(n, cin, h, w, cout, k, stride):
     _case(n, cin, h, w, cout, k, stride, residual=False)
@@ -50,6 +52,16 @@ def test_conv2d(n, cin, h, w, cout, k, stride):
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv2d_residual(k):
     _case(2, 640, 8, 8, 640, k, 1, residual=True, seed=1)
+
+
+def test_conv2d_splitk_residual():
+    from vp2p import ops, _lib
+    import ctypes
+    _case(32, 1280, 8, 8, 1280, 3, 1, residual=True, seed=2)
+    x = torch.empty(32, 1280, 8, 8, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.empty(1280, 1280, 3, 3, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a, _ = ops._conv_args(x, w, None, None, None, 1, 1)
+    assert _lib.load().vp2p_conv2d_workspace_bytes(ctypes.byref(a)) > 0     # the split path ran
 
 
 def test_conv2d_unsupported_raises():

@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
@@ -28,7 +28,7 @@ EXPORTS = ("vp2p_frame_attn_fwd", "vp2p_cross_kv_workspace_bytes", "vp2p_cross_k
            "vp2p_frame_attn_bwd_workspace_bytes", "vp2p_frame_attn_bwd", "vp2p_temporal_attn_bwd",
            "vp2p_group_norm_bwd_reduce", "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd",
            "vp2p_nulltext_loss", "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
-           "vp2p_add_layer_norm_fwd")
+           "vp2p_add_layer_norm_fwd", "vp2p_conv2d_workspace_bytes")
 
 
 class GroupNormArgs(ctypes.Structure):
@@ -43,7 +43,7 @@ class ConvArgs(ctypes.Structure):
                 ("batch", c_int32), ("in_h", c_int32), ("in_w", c_int32), ("cin", c_int32),
                 ("cout", c_int32), ("out_h", c_int32), ("out_w", c_int32),
                 ("kernel", c_int32), ("stride", c_int32), ("pad", c_int32), ("dtype", c_int32),
-                ("epilogue", c_int32)]
+                ("epilogue", c_int32), ("workspace", c_void_p), ("ksplit", c_int32)]
 
 
 class LayerNormArgs(ctypes.Structure):
@@ -167,6 +167,8 @@ def load(path: str = None):
     lib.vp2p_nulltext_loss_partials.argtypes = []
     lib.vp2p_conv2d_supported.argtypes = [POINTER(ConvArgs)]
     lib.vp2p_conv2d_fwd.argtypes = [POINTER(ConvArgs), c_void_p]
+    lib.vp2p_conv2d_workspace_bytes.argtypes = [POINTER(ConvArgs)]
+    lib.vp2p_conv2d_workspace_bytes.restype = c_int64
     lib.vp2p_add_layer_norm_fwd.argtypes = [POINTER(LayerNormArgs), c_void_p, c_void_p, c_void_p]
     for name in ("vp2p_frame_attn_fwd", "vp2p_cross_kv_prep", "vp2p_cross_attn_p2p_fwd",
                  "vp2p_temporal_attn_p2p_fwd", "vp2p_step_fused", "vp2p_abi_version",

@@ -511,7 +511,13 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
             residual = residual.contiguous(memory_format=torch.channels_last)
         a.residual = _ptr(residual)
     a.y = _ptr(y)
-    check(_lib.load().vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd")
+    lib = _lib.load()
+    wsb = lib.vp2p_conv2d_workspace_bytes(ctypes.byref(a))
+    ws = None
+    if wsb > 0:      # split-K slices (small-M shapes); from the caching allocator, no sync
+        ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
+        a.workspace = _ptr(ws)
+    check(lib.vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd")
     return y
 
 
