@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 4
+#define VP2P_ABI_VERSION 5
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -309,6 +309,8 @@ typedef struct vp2p_conv_args {
   int32_t epilogue;         /* vp2p_conv_epilogue */
   float* workspace;         /* fp32 split-K slices, vp2p_conv2d_workspace_bytes() bytes, or NULL (one pass) */
   int32_t ksplit;           /* set by the library; callers leave 0 */
+  int32_t upsample;         /* 1: x is (batch, in_h/2, in_w/2, cin), nearest-upsampled x2 on the fly
+                               (Upsample3D's F.interpolate, resnet.py:79-99); stride 1 only */
 } vp2p_conv_args;
 
 int vp2p_conv2d_supported(const vp2p_conv_args* args);

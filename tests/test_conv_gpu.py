@@ -92,3 +92,36 @@ def test_linear_geglu(M, K, inner):
     assert out.shape == (M, inner)
     err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("n,cin,h,w,cout", [(2, 1280, 8, 8, 1280), (3, 640, 5, 7, 640)])
+def test_conv2d_fused_upsample(n, cin, h, w, cout):
+    """K10 reading a x2 nearest upsample on the fly == F.interpolate then the conv (fp32 reference)."""
+    from vp2p import ops
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, cin, h, w, generator=g).to(torch.bfloat16).to(DEV).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5).to(torch.bfloat16).to(DEV)
+    wt = wt.contiguous(memory_format=torch.channels_last)
+    b = (torch.randn(cout, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    ref = F.conv2d(F.interpolate(x.float(), scale_factor=2.0, mode="nearest"), wt.float(), b.float(), 1, 1)
+    assert ops.conv2d_supported(x, wt, 1, 1, upsample=True)
+    out = ops.conv2d(x, wt, b, 1, 1, upsample=True)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
+
+
+def test_linear_residual():
+    from vp2p import ops
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(3, 500, 640, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(640, 640, generator=g) / 640 ** 0.5).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(640, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    r = torch.randn(3, 500, 640, generator=g).to(torch.bfloat16).to(DEV)
+    ref = F.linear(x.float(), w.float(), b.float()).to(torch.bfloat16).float() + r.float()
+    assert ops.linear_residual_supported(x, w, r)
+    out = ops.linear_residual(x, w, b, r)
+    torch.cuda.synchronize()
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err

@@ -119,7 +119,12 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
     for (int i = 0; i < G_ADMA; ++i) {
       const int iy = a_iy[i] + kh, ix = a_ix[i] + kw;
       const bool ok = a_ok[i] && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
-      const bf16* src = ok ? x + (((int64_t)a_n[i] * a.in_h + iy) * a.in_w + ix) * a.cin + c0 + a_c[i] : zero;
+      // upsample = 1: the input is nearest-upsampled x2 on the fly (Upsample3D, resnet.py:79-99):
+      // (iy, ix) of the virtual in_h x in_w image reads source pixel (iy/2, ix/2)
+      const int up = a.upsample;
+      const bf16* src = ok ? x + (((int64_t)a_n[i] * (a.in_h >> up) + (iy >> up)) * (a.in_w >> up) + (ix >> up)) *
+                                     a.cin + c0 + a_c[i]
+                           : zero;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
                                        16, 0, 0);
     }
@@ -292,6 +297,7 @@ extern "C" int vp2p_conv2d_supported(const vp2p_conv_args* a) {
   if (a->out_w != (a->in_w + 2 * a->pad - a->kernel) / a->stride + 1) return 0;
   if (a->epilogue != VP2P_CONV_EPI_NONE &&
       (a->epilogue != VP2P_CONV_EPI_GEGLU || a->kernel != 1 || a->stride != 1 || a->residual)) return 0;
+  if (a->upsample != 0 && (a->upsample != 1 || a->stride != 1 || (a->in_h & 1) || (a->in_w & 1))) return 0;
   return 1;
 }
 

@@ -469,17 +469,23 @@ def geglu_bwd(h: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
     return dh
 
 
-def _conv_args(x: torch.Tensor, weight: torch.Tensor, bias, residual, y, stride: int, padding: int):
+def _conv_args(x: torch.Tensor, weight: torch.Tensor, bias, residual, y, stride: int, padding: int,
+               upsample: bool = False):
     N, Cin, H, W = x.shape
+    if upsample:
+        H, W = 2 * H, 2 * W
     Cout, _, KH, KW = weight.shape
     Ho = (H + 2 * padding - KH) // stride + 1
     Wo = (W + 2 * padding - KW) // stride + 1
     dt = _lib.BF16 if x.dtype == torch.bfloat16 else -1
-    return _lib.ConvArgs(_ptr(x), _ptr(weight), _ptr(bias), _ptr(residual), _ptr(y), N, H, W, Cin, Cout, Ho, Wo,
-                         KH if KH == KW else -1, stride, padding, dt), (N, Cout, Ho, Wo)
+    a = _lib.ConvArgs(_ptr(x), _ptr(weight), _ptr(bias), _ptr(residual), _ptr(y), N, H, W, Cin, Cout, Ho, Wo,
+                      KH if KH == KW else -1, stride, padding, dt)
+    a.upsample = 1 if upsample else 0
+    return a, (N, Cout, Ho, Wo)
 
 
-def conv2d_supported(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0) -> bool:
+def conv2d_supported(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0,
+                     upsample: bool = False) -> bool:
     """True when K10 covers this convolution: bf16, channels-last, 1x1 / 3x3 'same' padding, stride
     1 or 2, Cin % 64 == 0, Cout % 160 == 0 (every resnet / up/down-sample conv of the SD-1.5 UNet
     except conv_in / conv_out)."""
@@ -487,12 +493,12 @@ def conv2d_supported(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad
         return False
     if not x.is_contiguous(memory_format=torch.channels_last):
         return False
-    a, _ = _conv_args(x, weight, None, None, None, stride, padding)
+    a, _ = _conv_args(x, weight, None, None, None, stride, padding, upsample)
     return bool(_lib.load().vp2p_conv2d_supported(ctypes.byref(a)))
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
-           padding: int = 0, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+           padding: int = 0, residual: Optional[torch.Tensor] = None, upsample: bool = False) -> torch.Tensor:
     """K10: nn.Conv2d on channels-last bf16 with the bias and an optional residual add fused
     (``residual + conv(x)``, the resnet shortcut add of resnet.py:196-205).  Returns a channels-last
     (N, Cout, Ho, Wo) tensor.  Raises for shapes K10 does not cover (see ``conv2d_supported``)."""
@@ -502,7 +508,7 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
         weight.contiguous(memory_format=torch.channels_last)
     if bias is not None and (bias.dtype != x.dtype or not bias.is_contiguous()):
         bias = bias.to(x.dtype).contiguous()
-    a, shape = _conv_args(x, w, bias, None, None, stride, padding)
+    a, shape = _conv_args(x, w, bias, None, None, stride, padding, upsample)
     y = torch.empty(shape, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
     if residual is not None:
         if residual.shape != y.shape or residual.dtype != y.dtype:
@@ -541,16 +547,17 @@ class ConvSelector:
             self.choice[key] = use
         return use
 
-    def run(self, x, weight, bias, stride: int, padding: int, residual, library):
+    def run(self, x, weight, bias, stride: int, padding: int, residual, library, upsample: bool = False):
         def k10():
-            return conv2d(x, weight, bias, stride, padding, residual=residual)
+            return conv2d(x, weight, bias, stride, padding, residual=residual, upsample=upsample)
 
         def lib():
             y = library()
             return y if residual is None else residual + y
 
-        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, residual is not None, x.device.index)
-        if self.pick(key, conv2d_supported(x, weight, stride, padding), k10, lib):
+        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, residual is not None, upsample,
+               x.device.index)
+        if self.pick(key, conv2d_supported(x, weight, stride, padding, upsample), k10, lib):
             return k10()
         return lib()
 
@@ -606,3 +613,35 @@ def linear_geglu(x: torch.Tensor, w_il: torch.Tensor, b_il: Optional[torch.Tenso
                       _lib.BF16, _lib.CONV_EPI_GEGLU)
     check(_lib.load().vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd(geglu)")
     return y
+
+
+def linear_residual(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                    residual: torch.Tensor) -> torch.Tensor:
+    """residual + x @ W^T + b on K10's GEMM core (a 1x1 convolution over M = rows pixels), the add
+    fused into the epilogue.  x: (..., K) contiguous bf16; residual: (..., N) contiguous."""
+    K = x.shape[-1]
+    M = x.numel() // K
+    N = weight.shape[0]
+    y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
+    a = _lib.ConvArgs(_ptr(x), _ptr(weight), _ptr(bias), _ptr(residual), _ptr(y), 1, M, 1, K, N, M, 1, 1, 1, 0,
+                      _lib.BF16, _lib.CONV_EPI_NONE)
+    lib = _lib.load()
+    ws = None
+    wsb = lib.vp2p_conv2d_workspace_bytes(ctypes.byref(a))
+    if wsb > 0:
+        ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
+        a.workspace = _ptr(ws)
+    check(lib.vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd(linear)")
+    return y
+
+
+def linear_residual_supported(x: torch.Tensor, weight: torch.Tensor, residual: torch.Tensor) -> bool:
+    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or not x.is_cuda:
+        return False
+    if not (x.is_contiguous() and weight.is_contiguous() and residual.is_contiguous()):
+        return False
+    K = x.shape[-1]
+    M = x.numel() // K
+    a = _lib.ConvArgs(None, None, None, None, None, 1, M, 1, K, weight.shape[0], M, 1, 1, 1, 0,
+                      _lib.BF16, _lib.CONV_EPI_NONE)
+    return bool(_lib.load().vp2p_conv2d_supported(ctypes.byref(a)))

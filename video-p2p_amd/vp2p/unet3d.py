@@ -235,7 +235,23 @@ class Transformer3DModel(nn.Module):
         tok = F.linear(tok, self.proj_in.weight.view(self.proj_in.out_channels, -1), self.proj_in.bias)
         for blk in self.transformer_blocks:
             tok = blk(tok, context, frames)
-        tok = F.linear(tok, self.proj_out.weight.view(self.proj_out.out_channels, -1), self.proj_out.bias)
+        w_out = self.proj_out.weight.view(self.proj_out.out_channels, -1)
+        if not torch.is_grad_enabled() and x.is_contiguous(memory_format=torch.channels_last):
+            # proj_out + the block's outer residual (attention.py:129-136) as one K10 GEMM where that
+            # measures faster than hipBLASLt + a separate add
+            res = x.permute(0, 2, 3, 1).reshape(Bf, H * W, C)        # the same bytes, no copy
+
+            def fused():
+                return ops.linear_residual(tok, w_out, self.proj_out.bias, res)
+
+            def lib():
+                return F.linear(tok, w_out, self.proj_out.bias) + res
+
+            key = ("proj_out", tuple(tok.shape), tuple(w_out.shape), x.device.index)
+            ok = ops.linear_residual_supported(tok, w_out, res)
+            out = fused() if ops.CONV.pick(key, ok, fused, lib) else lib()
+            return out.reshape(Bf, H, W, C).permute(0, 3, 1, 2)
+        tok = F.linear(tok, w_out, self.proj_out.bias)
         return tok.reshape(Bf, H, W, C).permute(0, 3, 1, 2) + x
 
 
@@ -254,6 +270,14 @@ class Upsample3D(nn.Module):
         self.conv = InflatedConv3d(channels, channels, 3, padding=1)
 
     def forward(self, x, size=None):
+        conv = self.conv
+        if size is None and not autograd.needs_grad(x, conv.weight) and x.is_contiguous(memory_format=torch.channels_last):
+            # the x2 nearest upsample read on the fly by K10 (the 4x tensor is never written), or
+            # interpolate + conv, whichever measured faster for this shape
+            def library():
+                up = F.interpolate(x, scale_factor=2.0, mode="nearest")
+                return nn.Conv2d.forward(conv, up.contiguous(memory_format=torch.channels_last))
+            return ops.CONV.run(x, conv.weight, conv.bias, conv.stride[0], conv.padding[0], None, library, upsample=True)
         if size is None:
             x = F.interpolate(x, scale_factor=2.0, mode="nearest")
         else:
