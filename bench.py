@@ -33,6 +33,16 @@ PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 RABBIT = (["a rabbit is jumping on the grass", "a origami rabbit is jumping on the grass"],
           False, (("rabbit",), ("rabbit",)), {"words": ["origami"], "values": [2]}, 0.2, 0.5)
+# The other reference edits (configs/*-p2p.yaml; cross 0.2 / self 0.5 are run_videop2p.py's defaults).
+EDITS = {
+    "rabbit": ("rabbit-jump-p2p", "AttentionRefine+LocalBlend+Reweight", RABBIT),
+    "penguin": ("penguin-run-p2p", "AttentionRefine+LocalBlend+Reweight",
+                (["a penguin is running on the ice", "a crochet penguin is running on the ice"],
+                 False, (("penguin",), ("penguin",)), {"words": ["crochet"], "values": [4]}, 0.2, 0.5)),
+    "car": ("car-drive-p2p", "AttentionReplace+LocalBlend+Reweight",
+            (["a car is driving on the road", "a car is driving on the railway"],
+             True, (("road",), ("railway",)), {"words": ["railway"], "values": [2]}, 0.2, 0.5)),
+}
 
 
 def parse():
@@ -41,6 +51,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=2, help="timed edits (each = 50 DDIM steps)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--edit", default="rabbit", choices=sorted(EDITS),
+                    help="which reference edit (configs/<name>-p2p.yaml): rabbit = configs[1] (default), "
+                         "penguin --frames 24 = configs[2], car = the word-swap AttentionReplace path")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--ddim-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -320,7 +333,7 @@ def main():
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     f = args.frames
-    prompts, swap, blend, eq, cross, self_ = RABBIT
+    edit_name, edit_kind, (prompts, swap, blend, eq, cross, self_) = EDITS[args.edit]
     tok = SyntheticCLIPTokenizer()
     unet = init_random_(UNet3DConditionModel(), seed=0).to(dev, dtype).to(memory_format=torch.channels_last)
     unet.eval()
@@ -386,7 +399,7 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "strong" if frames_mode else "weak", "vs_baseline": None,
         "dtype": args.dtype, "data": "synthetic (random-init SD-1.5-geometry UNet3D, random text embeddings, x_T~N(0,1))",
-        "config": {"workload": "rabbit-jump-p2p --fast: AttentionRefine+LocalBlend+Reweight, 8 frames 512^2, "
+        "config": {"workload": f"{edit_name} --fast: {edit_kind}, {f} frames 512^2, "
                                f"{args.ddim_steps}-step DDIM, UNet batch 4", "frames": f, "resolution": 512,
                    "ddim_steps": args.ddim_steps, "unet_batch": 4,
                    "parallelism": f"frame-sharded x{world} (RCCL)" if frames_mode else f"clip-parallel x{world}"},
