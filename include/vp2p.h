@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 5
+#define VP2P_ABI_VERSION 6
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -120,6 +120,9 @@ typedef struct vp2p_cross_attn_args {
   /* Optional post-edit probabilities in the reference's attn layout
    * ((batch*frames*heads), tokens_q, tokens_kv) fp32.  NULL = off. */
   float* probs_out;
+  /* Scratch for the per-head LocalBlend partials, (prompts, heads, frames*tokens_q) fp32; required
+   * when lb_acc is set (the head sum is finished in a fixed order by a second pass). */
+  float* lb_ws;
 } vp2p_cross_attn_args;
 
 /* Bytes of the K/V workspace for one context of the given shape (<0: unsupported). */

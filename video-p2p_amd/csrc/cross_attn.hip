@@ -14,7 +14,7 @@
 //        layers (:131-146), so this kernel accumulates exactly that reduction (lb_acc) instead.
 //
 // The reference materialises probs (B*f*h, N, 77) and makes ~6-8 elementwise passes over them.
-// Here one workgroup owns 32 query tokens of one CFG half for all heads and prompts: the source
+// Here one wave owns 32 query tokens x one head of one CFG half for all its prompts: the source
 // prompt's probabilities are parked in LDS (fp32) while the edited prompts are computed, so the
 // edit is a handful of LDS reads per word and nothing but Q in / O out touches HBM.
 // The 77-token K/V (identical for all frames: attention.py:95 repeats the context per frame) are
@@ -32,6 +32,7 @@ struct CrossCfg {
   static constexpr int KS = DP / KD;
   static constexpr int DV = round_up(D, 32);
   static constexpr int NT = DV / 32;
+  static constexpr int OCC = !BF ? 1 : (D <= 80 ? 3 : 2);   // waves/SIMD requested (no spills at 3 for these)
 };
 
 // Workspace layout for KB key blocks (KP = 32*KB padded keys), per (b, head):
@@ -84,206 +85,253 @@ __global__ void cross_kv_prep_kernel(const T* __restrict__ k, const T* __restric
   }
 }
 
+// One wave owns one (CFG half, 32-query block, head) item at a time and walks the half's prompts in
+// order, so the source prompt's probabilities (parked in the wave's LDS rows) are there when the
+// edited prompts need them.  A workgroup (4 waves = 4 heads) of CFG half blockIdx.y takes items
+// blockIdx.x, + gridDim.x, ..., and every wave fetches the next (item, prompt)'s Q fragments while
+// the current one computes.  Waves never synchronise after the table staging; the
+// LocalBlend head sum is finished by cross_lb_reduce_kernel from per-head partials, in head order.
 template <typename T, int D, int KB>
-__global__ __launch_bounds__(256) void cross_attn_kernel(const vp2p_cross_attn_args a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CrossCfg<T, D>::OCC, 8)))
+void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
   using M = Mfma<T>;
   using C = CrossCfg<T, D>;
   constexpr int KP = 32 * KB;
-  constexpr int PROW = KP + 1;                 // fp32 source-prob row in LDS (odd: conflict-free)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* psrc_all = reinterpret_cast<float*>(smem);                 // [4 waves][32][PROW]
-  float* lbred = psrc_all + 4 * 32 * PROW;                          // [4 waves][4 prompts][32]
 
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int FQ = a.frames * a.tokens_q;
   const int qblocks = (FQ + 31) >> 5;
+  const int hgroups = (a.heads + 3) >> 2;
+  const int items = qblocks * hgroups;
   const bool p2p = a.prompts > 0 && a.batch == 2 * a.prompts;
   const int RP = p2p ? a.prompts : 1;          // rows per group
-  const int g = blockIdx.x / qblocks;          // group: CFG half (p2p) or batch row
-  const int qb = blockIdx.x - g * qblocks;
+  const int g = blockIdx.y;                    // group: CFG half (p2p) or batch row
   const bool cond = p2p && g == 1;
   const bool edit = cond && (a.edit_mode != VP2P_EDIT_NONE || a.reweight);
   const bool lb = cond && a.lb_acc != nullptr;
   const int NKV = a.tokens_kv;
 
-  const int qi = qb * 32 + r;
-  const bool qv = qi < FQ;
-  const int fr = qv ? qi / a.tokens_q : 0;
-  const int pos = qv ? qi - fr * a.tokens_q : 0;
-  float* psrc = psrc_all + w * 32 * PROW + r * PROW;
+  float* psrc = reinterpret_cast<float*>(smem) + (w * 32 + r) * prow;
+  // The edit tables of this CFG half, staged once per workgroup (every lane of a 32-lane half reads
+  // the same word, so these are broadcast LDS reads): per edited prompt and word
+  // {refine alpha, equalizer, alpha_t, source word}, and LocalBlend's word weights per prompt.
+  f32x4* etab = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem) + 4 * 32 * prow);
+  float* lbw = reinterpret_cast<float*>(etab + (a.prompts > 1 ? (a.prompts - 1) * NKV : 0));
+  if (edit) {
+    for (int i = tid; i < (RP - 1) * NKV; i += 256) {
+      const int wd = i % NKV;
+      f32x4 t;
+      t[0] = a.edit_mode == VP2P_EDIT_REFINE ? a.refine_alpha[i] : 0.f;
+      t[1] = a.reweight ? a.equalizer[wd] : 1.f;
+      t[2] = a.alpha_words[i];
+      t[3] = __int_as_float(a.edit_mode == VP2P_EDIT_REFINE ? a.map_idx[i] : wd);
+      etab[i] = t;
+    }
+  }
+  if (lb)
+    for (int i = tid; i < RP * NKV; i += 256) lbw[i] = a.lb_word_alpha[i];
+  if (edit || lb) __syncthreads();
+
   const float cs = a.scale * kLog2e;
   const T* ws = static_cast<const T*>(a.kv_ws);
   const int64_t kelems = (int64_t)a.batch * a.heads * KP * C::DP;
 
-  float lbsum[4] = {0.f, 0.f, 0.f, 0.f};
+  // Q fragments of (item, prompt p); zero for padded queries / heads
+  auto load_q = [&](int item, int p, typename M::frag* dst) {
+    const int qb = item / hgroups, head = (item - qb * hgroups) * 4 + w;
+    const int qi = qb * 32 + r;
+    const bool ok = qi < FQ && head < a.heads;
+    const int fr = ok ? qi / a.tokens_q : 0;
+    const int pos = ok ? qi - fr * a.tokens_q : 0;
+    const T* row = static_cast<const T*>(a.q) + (g * RP + p) * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * D;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) dst[s] = ok ? M::row_frag(row, s, h, D) : M::zero();
+  };
 
-  for (int head = w; head < a.heads; head += 4) {
-    for (int p = 0; p < RP; ++p) {
-      const int b = g * RP + p;
-      const T* qrow = static_cast<const T*>(a.q) + b * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * D;
-      typename M::frag qf[C::KS];
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) qf[s] = qv ? M::row_frag(qrow, s, h, D) : M::zero();
+  typename M::frag qn[C::KS];
+  if (blockIdx.x < items) load_q(blockIdx.x, 0, qn);
 
-      const T* kb_base = ws + ((int64_t)(b * a.heads + head) * KP) * C::DP;
-      f32x16 sc[KB];
+  for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    const int qb = item / hgroups;
+    const int head = (item - qb * hgroups) * 4 + w;
+    const bool hv = head < a.heads;
+    const int qi = qb * 32 + r;
+    const bool qv = qi < FQ && hv;
+    const int fr = qv ? qi / a.tokens_q : 0;
+    const int pos = qv ? qi - fr * a.tokens_q : 0;
+    const int hs = hv ? head : 0;              // padded heads compute on head 0's K/V, store nothing
+  for (int p = 0; p < RP; ++p) {
+    const int b = g * RP + p;
+    typename M::frag qf[C::KS];
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        sc[kb] = zero16();
-        const T* krow = kb_base + (kb * 32 + r) * C::DP;
+    for (int s = 0; s < C::KS; ++s) qf[s] = qn[s];
+    if (p + 1 < RP) load_q(item, p + 1, qn);
+    else if (item + (int)gridDim.x < items) load_q(item + gridDim.x, 0, qn);
+
+    const T* kb_base = ws + ((int64_t)(b * a.heads + hs) * KP) * C::DP;
+    f32x16 sc[KB];
 #pragma unroll
-        for (int s = 0; s < C::KS; ++s) {
-          typename M::frag af;
-          if constexpr (C::BF) af = *reinterpret_cast<const bf16x8*>(krow + 16 * s + 8 * h);
-          else af = krow[2 * s + h];
-          sc[kb] = M::mma(af, qf[s], sc[kb]);
-        }
+    for (int kb = 0; kb < KB; ++kb) {
+      sc[kb] = zero16();
+      const T* krow = kb_base + (kb * 32 + r) * C::DP;
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        typename M::frag af;
+        if constexpr (C::BF) af = *reinterpret_cast<const bf16x8*>(krow + 16 * s + 8 * h);
+        else af = krow[2 * s + h];
+        sc[kb] = M::mma(af, qf[s], sc[kb]);
       }
-      // row softmax over the valid keys (the reference's global max gives the same probabilities
-      // wherever it does not underflow: ptp_utils.py:217)
-      float mx = kNegInf;
+    }
+    // row softmax over the valid keys (the reference's global max gives the same probabilities
+    // wherever it does not underflow: ptp_utils.py:217)
+    float mx = kNegInf;
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+    for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float v = (kb * 32 + acc_row(i, h) < NKV) ? sc[kb][i] * cs : kNegInf;
-          sc[kb][i] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, xhalf(mx));
-      float sum = 0.f;
+      for (int i = 0; i < 16; ++i) {
+        const float v = (kb * 32 + acc_row(i, h) < NKV) ? sc[kb][i] * cs : kNegInf;
+        sc[kb][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, xhalf(mx));
+    float sum = 0.f;
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+    for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float e = fast_exp2(sc[kb][i] - mx);
-          sc[kb][i] = e;
-          sum += e;
-        }
-      sum += xhalf(sum);
-      const float inv = 1.f / sum;
+      for (int i = 0; i < 16; ++i) {
+        const float e = fast_exp2(sc[kb][i] - mx);
+        sc[kb][i] = e;
+        sum += e;
+      }
+    sum += xhalf(sum);
+    const float inv = 1.f / sum;
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+    for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sc[kb][i] *= inv;
+      for (int i = 0; i < 16; ++i) sc[kb][i] *= inv;
 
-      if (edit) {
-        if (p == 0) {
+    if (edit) {
+      if (p == 0) {
 #pragma unroll
-          for (int kb = 0; kb < KB; ++kb)
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) psrc[kb * 32 + acc_row(i, h)] = sc[kb][i];
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else {
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) psrc[wd] = sc[kb][i];
+          }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else {
 #pragma clang fp contract(off)
-          const int pe = p - 1;
+        const int pe = p - 1;
 #pragma unroll
-          for (int kb = 0; kb < KB; ++kb)
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int wd = kb * 32 + acc_row(i, h);
-              if (wd < NKV) {
-                const float pe_val = sc[kb][i];
-                float R;
-                if (a.edit_mode == VP2P_EDIT_REPLACE) {
-                  const int* ptr = a.map_ptr + pe * (NKV + 1);
-                  float gsum = 0.f;
-                  for (int n = ptr[wd]; n < ptr[wd + 1]; ++n) gsum += psrc[a.map_idx[n]] * a.map_val[n];
-                  R = gsum;
-                } else if (a.edit_mode == VP2P_EDIT_REFINE) {
-                  const float ra = a.refine_alpha[pe * NKV + wd];
-                  const float gth = psrc[a.map_idx[pe * NKV + wd]];
-                  R = gth * ra + pe_val * (1.f - ra);
-                } else {
-                  R = psrc[wd];
-                }
-                if (a.reweight) R = R * a.equalizer[wd];
-                const float aw = a.alpha_words[pe * NKV + wd];
-                sc[kb][i] = R * aw + (1.f - aw) * pe_val;
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) {
+              const float pe_val = sc[kb][i];
+              const f32x4 t = etab[pe * NKV + wd];
+              float R;
+              if (a.edit_mode == VP2P_EDIT_REPLACE) {
+                const int* ptr = a.map_ptr + pe * (NKV + 1);
+                float gsum = 0.f;
+                for (int n = ptr[wd]; n < ptr[wd + 1]; ++n) gsum += psrc[a.map_idx[n]] * a.map_val[n];
+                R = gsum;
+              } else if (a.edit_mode == VP2P_EDIT_REFINE) {
+                R = psrc[__float_as_int(t[3])] * t[0] + pe_val * (1.f - t[0]);
+              } else {
+                R = psrc[wd];
               }
+              R = R * t[1];             // equalizer (1 without Reweight: exact)
+              sc[kb][i] = R * t[2] + (1.f - t[2]) * pe_val;
             }
-        }
-      }
-      if (lb) {
-        float part = 0.f;
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int wd = kb * 32 + acc_row(i, h);
-            if (wd < NKV) part += a.lb_word_alpha[p * NKV + wd] * sc[kb][i];
-          }
-        lbsum[p & 3] += part + xhalf(part);
-      }
-      if (a.probs_out && qv) {
-        float* prow = a.probs_out + ((((int64_t)b * a.frames + fr) * a.heads + head) * a.tokens_q + pos) * NKV;
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int wd = kb * 32 + acc_row(i, h);
-            if (wd < NKV) prow[wd] = sc[kb][i];
           }
       }
-
-      // O^T = V^T P^T over the padded keys (P is exactly 0 there)
-      const T* vb_base = ws + kelems + ((int64_t)(b * a.heads + head) * KP) * C::DV;
-      f32x16 o[C::NT];
-#pragma unroll
-      for (int t = 0; t < C::NT; ++t) o[t] = zero16();
+    }
+    if (lb) {  // this head's word-weighted map of token qi -> lb_ws[p][head][qi]
+      float part = 0.f;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int sp = 0; sp < M::PV_STEPS; ++sp) {
-          const typename M::frag pf = M::p_frag(sc[kb], sp);
-#pragma unroll
-          for (int t = 0; t < C::NT; ++t) {
-            typename M::frag vf;
-            if constexpr (C::BF)
-              vf = *reinterpret_cast<const bf16x8*>(vb_base + (int64_t)(32 * t + r) * KP + kb * 32 + 16 * sp + 8 * h);
-            else
-              vf = vb_base[(int64_t)(kb * 32 + f32_pv_key(sp, h)) * C::DV + 32 * t + r];
-            o[t] = M::mma(vf, pf, o[t]);
-          }
+        for (int i = 0; i < 16; ++i) {
+          const int wd = kb * 32 + acc_row(i, h);
+          if (wd < NKV) part += lbw[p * NKV + wd] * sc[kb][i];
         }
-      if (qv) {
-        T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
+      part += xhalf(part);
+      if (h == 0 && qv) a.lb_ws[((int64_t)p * a.heads + head) * FQ + qi] = part;
+    }
+    if (a.probs_out && qv) {
+      float* prow_out = a.probs_out + ((((int64_t)b * a.frames + fr) * a.heads + head) * a.tokens_q + pos) * NKV;
 #pragma unroll
-        for (int t = 0; t < C::NT; ++t)
+      for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const int dc = 32 * t + 8 * gq + 4 * h;
-            if (dc < D) {
-              if constexpr (C::BF) {
-                bf16x4 v;
+        for (int i = 0; i < 16; ++i) {
+          const int wd = kb * 32 + acc_row(i, h);
+          if (wd < NKV) prow_out[wd] = sc[kb][i];
+        }
+    }
+
+    // O^T = V^T P^T over the padded keys (P is exactly 0 there)
+    const T* vb_base = ws + kelems + ((int64_t)(b * a.heads + hs) * KP) * C::DV;
+    f32x16 o[C::NT];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (bf16)o[t][4 * gq + j];
-                *reinterpret_cast<bf16x4*>(orow + dc) = v;
-              } else {
-                f32x4 v;
+    for (int t = 0; t < C::NT; ++t) o[t] = zero16();
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = o[t][4 * gq + j];
-                *reinterpret_cast<f32x4*>(orow + dc) = v;
-              }
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int sp = 0; sp < M::PV_STEPS; ++sp) {
+        const typename M::frag pf = M::p_frag(sc[kb], sp);
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t) {
+          typename M::frag vf;
+          if constexpr (C::BF)
+            vf = *reinterpret_cast<const bf16x8*>(vb_base + (int64_t)(32 * t + r) * KP + kb * 32 + 16 * sp + 8 * h);
+          else
+            vf = vb_base[(int64_t)(kb * 32 + f32_pv_key(sp, h)) * C::DV + 32 * t + r];
+          o[t] = M::mma(vf, pf, o[t]);
+        }
+      }
+    if (qv) {
+      T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int dc = 32 * t + 8 * gq + 4 * h;
+          if (dc < D) {
+            if constexpr (C::BF) {
+              bf16x4 v;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (bf16)o[t][4 * gq + j];
+              *reinterpret_cast<bf16x4*>(orow + dc) = v;
+            } else {
+              f32x4 v;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = o[t][4 * gq + j];
+              *reinterpret_cast<f32x4*>(orow + dc) = v;
             }
           }
-      }
+        }
     }
   }
+  }
+}
 
-  if (lb) {  // deterministic head reduction across the 4 waves; one read-modify-write per token
-    if (h == 0)
-      for (int p = 0; p < RP && p < 4; ++p) lbred[(w * 4 + p) * 32 + r] = lbsum[p];
-    __syncthreads();
-    if (w == 0 && h == 0 && qv) {
-      for (int p = 0; p < RP && p < 4; ++p) {
-        const float tot = lbred[(0 * 4 + p) * 32 + r] + lbred[(1 * 4 + p) * 32 + r] +
-                          lbred[(2 * 4 + p) * 32 + r] + lbred[(3 * 4 + p) * 32 + r];
-        a.lb_acc[((int64_t)p * a.frames + fr) * a.tokens_q + pos] += tot;
-      }
-    }
+// lb_acc[p][qi] += sum over heads (in head order) of lb_ws[p][head][qi]: deterministic, one
+// read-modify-write per (prompt, token).
+__global__ void cross_lb_reduce_kernel(float* __restrict__ lb_acc, const float* __restrict__ lb_ws,
+                                       int prompts, int heads, int fq) {
+  const int64_t n = (int64_t)prompts * fq;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(i / fq);
+    const int64_t qi = i - (int64_t)p * fq;
+    const float* src = lb_ws + (int64_t)p * heads * fq + qi;
+    float tot = 0.f;
+    for (int hd = 0; hd < heads; ++hd) tot += src[(int64_t)hd * fq];
+    lb_acc[i] += tot;
   }
 }
 
@@ -306,15 +354,30 @@ static int cross_pad_dims(int head_dim, int dtype, int& dp, int& dv) {
 
 template <typename T, int D, int KB>
 static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
-  constexpr int KP = 32 * KB;
   const int FQ = a->frames * a->tokens_q;
   const bool p2p = a->prompts > 0 && a->batch == 2 * a->prompts;
   const int groups = p2p ? 2 : a->batch;
-  const int64_t nwg = (int64_t)groups * ((FQ + 31) / 32);
-  if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-  const size_t lds = (4 * 32 * (KP + 1) + 4 * 4 * 32) * sizeof(float);
-  hipLaunchKernelGGL((cross_attn_kernel<T, D, KB>), dim3((unsigned)nwg), dim3(256), lds, s, *a);
-  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+  const int64_t items = (int64_t)((FQ + 31) / 32) * ((a->heads + 3) / 4);
+  if (items <= 0 || groups > 65535) return VP2P_E_SHAPE;
+  // One item per workgroup: measured faster at the UNet's shapes than a resident grid looping over
+  // items with cross-item Q prefetch (res-64 d40: 113 vs 132 us, profiles/r01_k2_ab.txt); the loop
+  // stays for grids beyond the 2^31 workgroup limit.
+  const int64_t nwg = std::min<int64_t>(items, 0x7fffffff);
+  const int prow = a->tokens_kv | 1;           // odd fp32 row stride: conflict-free per-lane rows
+  const int rp = p2p ? a->prompts : 1;
+  const size_t lds = (size_t)4 * 32 * prow * sizeof(float) + (size_t)(rp - 1) * a->tokens_kv * 16 +
+                     (size_t)rp * a->tokens_kv * sizeof(float);
+  hipLaunchKernelGGL((cross_attn_kernel<T, D, KB>), dim3((unsigned)nwg, (unsigned)groups), dim3(256), lds, s,
+                     *a, prow);
+  if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
+  if (p2p && a->lb_acc) {
+    const int64_t n = (int64_t)a->prompts * FQ;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(cross_lb_reduce_kernel, dim3(blocks), dim3(256), 0, s, a->lb_acc, a->lb_ws,
+                       a->prompts, a->heads, FQ);
+    if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
+  }
+  return VP2P_OK;
 }
 
 template <typename T, int D>
@@ -399,7 +462,7 @@ extern "C" int vp2p_cross_attn_p2p_fwd(const vp2p_cross_attn_args* a, void* stre
     if (a->edit_mode == VP2P_EDIT_REFINE && (!a->map_idx || !a->refine_alpha)) return VP2P_E_ARG;
     if (a->reweight && !a->equalizer) return VP2P_E_ARG;
   }
-  if (a->lb_acc && (!p2p || !a->lb_word_alpha)) return VP2P_E_ARG;
+  if (a->lb_acc && (!p2p || !a->lb_word_alpha || !a->lb_ws)) return VP2P_E_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
 #define VP2P_CROSS(DIM) \
   case DIM: return a->dtype == VP2P_BF16 ? launch_cross_kb<bf16, DIM>(a, s) : launch_cross_kb<float, DIM>(a, s);

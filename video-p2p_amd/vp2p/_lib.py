@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
@@ -88,7 +88,8 @@ class CrossAttnArgs(ctypes.Structure):
                 ("prompts", c_int32), ("edit_mode", c_int32), ("reweight", c_int32),
                 ("alpha_words", c_void_p), ("map_ptr", c_void_p), ("map_idx", c_void_p),
                 ("map_val", c_void_p), ("refine_alpha", c_void_p), ("equalizer", c_void_p),
-                ("lb_acc", c_void_p), ("lb_word_alpha", c_void_p), ("probs_out", c_void_p)]
+                ("lb_acc", c_void_p), ("lb_word_alpha", c_void_p), ("probs_out", c_void_p),
+                ("lb_ws", c_void_p)]
 
 
 class TemporalAttnArgs(ctypes.Structure):

@@ -222,7 +222,9 @@ def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frame
                            _ptr(plan.refine_alpha) if plan is not None else None,
                            _ptr(plan.equalizer) if plan is not None else None,
                            _ptr(lb_acc), _ptr(plan.lb_word_alpha) if (plan is not None and lb_acc is not None) else None,
-                           _ptr(probs_out))
+                           _ptr(probs_out),
+                           _ptr(torch.empty(P * heads * frames * N, device=q.device, dtype=torch.float32))
+                           if lb_acc is not None else None)
     check(_lib.load().vp2p_cross_attn_p2p_fwd(ctypes.byref(a), _stream()), "vp2p_cross_attn_p2p_fwd")
     return out
 
