@@ -85,10 +85,13 @@ static bool gn_geom(const vp2p_group_norm_args* a, GnGeom* g) {
   if (g->threads > 512) return false;
   g->cg = a->channels / a->groups;
   g->L = (int64_t)a->frames * a->rows;
-  // ~1024 blocks per launch, at most 16 rows per thread (4 rounds of kUnroll loads in flight)
+  if (g->L >= ((int64_t)1 << 31)) return false;
+  // ~1024 blocks per launch, 8..16 rows per thread (2..4 rounds of kUnroll loads in flight).  The
+  // floor of 8 keeps the partial count (which every apply block merges) small at the 8x8 / 16x16
+  // latents (171 -> 22 partials per group at 8x8x1280).
   const int64_t all = g->L * a->batch;
   int64_t rpt = (all + (int64_t)g->R * 1024 - 1) / ((int64_t)g->R * 1024);
-  if (rpt < 1) rpt = 1;
+  if (rpt < 8) rpt = 8;
   if (rpt > 16) rpt = 16;
   const int64_t chunk = rpt * g->R;
   g->chunk = (int)chunk;
@@ -105,7 +108,8 @@ __device__ __forceinline__ void load_row(const vp2p_group_norm_args& a, const T*
   V8<T>::load(x + row * a.channels, val);
   if (ADD) {
     float ad[8];
-    V8<T>::load(static_cast<const T*>(a.add) + ((int64_t)b * a.frames + row / a.rows) * a.channels + v * 8, ad);
+    const int fr = (int)((uint32_t)row / (uint32_t)a.rows);     // L = frames * rows < 2^31 (gn_geom)
+    V8<T>::load(static_cast<const T*>(a.add) + ((int64_t)b * a.frames + fr) * a.channels + v * 8, ad);
 #pragma unroll
     for (int j = 0; j < 8; ++j) val[j] = V8<T>::round(val[j] + ad[j]);
   }
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_arg
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = fmaf(val[j], sc[j], sh[j]);
-      if (SILU) t = t / (1.f + __expf(-t));
+      if (SILU) t = t * __builtin_amdgcn_rcpf(1.f + __expf(-t));   // v_rcp, not the IEEE divide sequence
       val[j] = t;
     }
   };
