@@ -303,8 +303,22 @@ def nulltext_main(args, world, rank, dev):
         print(json.dumps(result), flush=True)
 
 
+def _heartbeat(period=30.0):
+    """A line on stderr every `period` s, so a long run (first use of new conv shapes, 24 frames) is
+    never mistaken for a hung one."""
+    import threading
+
+    def beat():
+        t0 = time.perf_counter()
+        while True:
+            time.sleep(period)
+            print(f"[bench] running {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     args = parse()
+    _heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
