@@ -1,7 +1,11 @@
 """Interleaved A/B of the K2 cross-attention + P2P kernel: the in-tree library (B) against another
 build of it (A, --lib-a; e.g. the previous kernel saved before a change).  Both run the edit the
 bench runs (rabbit-jump AttentionRefine + Reweight, LocalBlend on at res-16) at the B4 f8 shapes;
-outputs are compared (bit-equal O expected; LocalBlend sums within float reassociation)."""
+outputs are compared (bit-equal O expected; LocalBlend sums within float reassociation).
+
+Caveat: two loaded builds whose kernels have the SAME mangled name launch one code object (the
+runtime resolves the kernel by name), so an A/B is only valid when the changed kernel's name or
+signature differs between the builds; the bit-equality / reference checks catch a mix-up."""
 import argparse
 import ctypes
 import json

@@ -34,12 +34,20 @@ struct TempCfg {
   static constexpr int WAVE_LDS = 32 * VROW * (int)sizeof(T);
 };
 
+// One wave owns one (CFG half, G-token block, head) and walks the half's prompts; heads are spread
+// over blockIdx.y.  For d <= 80 the next prompt's Q, K and V rows are fetched while the current
+// prompt computes (and the first prompt's V with its Q and K), so each wave exposes one HBM
+// latency instead of two per prompt.
 template <typename T, int D>
-__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void temporal_attn_kernel(const vp2p_temporal_attn_args a, int lf) {
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void temporal_attn_p2p_kernel(const vp2p_temporal_attn_args a, int lf) {
   using M = Mfma<T>;
   using C = TempCfg<T, D>;
+  constexpr bool PF = C::KS <= 5;
+  constexpr int VN = (C::CPR + 1) / 2;          // V vectors per lane (c = h, h + 2, ...)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int head = blockIdx.y * 4 + w;
+  if (head >= a.heads) return;
   T* Vs = reinterpret_cast<T*>(smem + w * C::WAVE_LDS);
   for (int i = l; i < C::WAVE_LDS / 16; i += 64) reinterpret_cast<u32x4*>(Vs)[i] = u32x4{0, 0, 0, 0};
 
@@ -58,115 +66,136 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void temporal_attn_ker
   const bool rv = fr < F && pos < N;
   const float cs = a.scale * kLog2e;
 
-  for (int head = w; head < a.heads; head += 4) {
-    typename M::frag psrc[M::PV_STEPS];
-    f32x16 prob_src;
-    for (int p = 0; p < RP; ++p) {
-      const int b = g * RP + p;
-      const int64_t qoff = rv ? b * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * D : 0;
-      const int64_t koff = rv ? b * a.k_sb + fr * a.k_sf + pos * a.k_sn + head * D : 0;
-      const int64_t voff = rv ? b * a.v_sb + fr * a.v_sf + pos * a.v_sn + head * D : 0;
-      f32x16 sc;
-      typename M::frag pf[M::PV_STEPS];
-      if (replace && p > 0) {
+  // operand rows of prompt p (Q, K only when its scores are computed, V always)
+  typename M::frag qn[C::KS], kn[C::KS];
+  u32x4 vn[VN];
+  auto load = [&](int p, typename M::frag* qd, typename M::frag* kd, u32x4* vd) {
+    const int b = g * RP + p;
+    if (!(replace && p > 0)) {
+      const T* qrow = static_cast<const T*>(a.q) + (rv ? b * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * D : 0);
+      const T* krow = static_cast<const T*>(a.k) + (rv ? b * a.k_sb + fr * a.k_sf + pos * a.k_sn + head * D : 0);
 #pragma unroll
-        for (int sp = 0; sp < M::PV_STEPS; ++sp) pf[sp] = psrc[sp];
-        sc = prob_src;
-      } else {
-        const T* qrow = static_cast<const T*>(a.q) + qoff;
-        const T* krow = static_cast<const T*>(a.k) + koff;
-        sc = zero16();
-#pragma unroll
-        for (int s = 0; s < C::KS; ++s) {
-          const typename M::frag qf = rv ? M::row_frag(qrow, s, h, D) : M::zero();
-          const typename M::frag kf = rv ? M::row_frag(krow, s, h, D) : M::zero();
-          sc = M::mma(kf, qf, sc);
-        }
-        float mx = kNegInf;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int kk = acc_row(i, h);
-          const bool ok = (kk >> lf) == slot && (kk & (fpad - 1)) < F;
-          const float v = ok ? sc[i] * cs : kNegInf;
-          sc[i] = v;
-          mx = fmaxf(mx, v);
-        }
-        mx = fmaxf(mx, xhalf(mx));
-        float sum = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float e = fast_exp2(sc[i] - mx);
-          sc[i] = e;
-          sum += e;
-        }
-        sum += xhalf(sum);
-        const float inv = 1.f / sum;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[i] *= inv;
-#pragma unroll
-        for (int sp = 0; sp < M::PV_STEPS; ++sp) pf[sp] = M::p_frag(sc, sp);
-        if (replace) {
-#pragma unroll
-          for (int sp = 0; sp < M::PV_STEPS; ++sp) psrc[sp] = pf[sp];
-          prob_src = sc;
-        }
+      for (int s = 0; s < C::KS; ++s) {
+        qd[s] = rv ? M::row_frag(qrow, s, h, D) : M::zero();
+        kd[s] = rv ? M::row_frag(krow, s, h, D) : M::zero();
       }
-      if (a.probs_out && rv) {
-        float* prow = a.probs_out + ((((int64_t)b * N + pos) * a.heads + head) * F + fr) * F;
+    }
+    const T* vrow = static_cast<const T*>(a.v) + (rv ? b * a.v_sb + fr * a.v_sf + pos * a.v_sn + head * D : 0);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int kk = acc_row(i, h);
-          if ((kk >> lf) == slot && (kk & (fpad - 1)) < F) prow[kk & (fpad - 1)] = sc[i];
-        }
-      }
+    for (int i = 0; i < VN; ++i) {
+      const int c = h + 2 * i;
+      vd[i] = (rv && c < C::CPR) ? *reinterpret_cast<const u32x4*>(vrow + c * C::EPC) : u32x4{0, 0, 0, 0};
+    }
+  };
+  if constexpr (PF) load(0, qn, kn, vn);
 
-      // stage this tile's 32 V rows (row index = lane row r) in the wave's LDS image
-      __builtin_amdgcn_wave_barrier();
-      {
-        const T* vrow = static_cast<const T*>(a.v) + voff;
-        for (int c = h; c < C::CPR; c += 2) {
-          const u32x4 val = rv ? *reinterpret_cast<const u32x4*>(vrow + c * C::EPC) : u32x4{0, 0, 0, 0};
-          *reinterpret_cast<u32x4*>(Vs + r * C::VROW + c * C::EPC) = val;
-        }
+  typename M::frag psrc[M::PV_STEPS];
+  f32x16 prob_src;
+  for (int p = 0; p < RP; ++p) {
+    const int b = g * RP + p;
+    typename M::frag qf[C::KS], kf[C::KS];
+    u32x4 vv[VN];
+    if constexpr (PF) {
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) { qf[s] = qn[s]; kf[s] = kn[s]; }
+#pragma unroll
+      for (int i = 0; i < VN; ++i) vv[i] = vn[i];
+      if (p + 1 < RP) load(p + 1, qn, kn, vn);
+    } else {
+      load(p, qf, kf, vv);
+    }
+    f32x16 sc;
+    typename M::frag pf[M::PV_STEPS];
+    if (replace && p > 0) {
+#pragma unroll
+      for (int sp = 0; sp < M::PV_STEPS; ++sp) pf[sp] = psrc[sp];
+      sc = prob_src;
+    } else {
+      sc = zero16();
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) sc = M::mma(kf[s], qf[s], sc);
+      float mx = kNegInf;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kk = acc_row(i, h);
+        const bool ok = (kk >> lf) == slot && (kk & (fpad - 1)) < F;
+        const float v = ok ? sc[i] * cs : kNegInf;
+        sc[i] = v;
+        mx = fmaxf(mx, v);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      mx = fmaxf(mx, xhalf(mx));
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = fast_exp2(sc[i] - mx);
+        sc[i] = e;
+        sum += e;
+      }
+      sum += xhalf(sum);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[i] *= inv;
+#pragma unroll
+      for (int sp = 0; sp < M::PV_STEPS; ++sp) pf[sp] = M::p_frag(sc, sp);
+      if (replace) {
+#pragma unroll
+        for (int sp = 0; sp < M::PV_STEPS; ++sp) psrc[sp] = pf[sp];
+        prob_src = sc;
+      }
+    }
+    if (a.probs_out && rv) {
+      float* prow = a.probs_out + ((((int64_t)b * N + pos) * a.heads + head) * F + fr) * F;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kk = acc_row(i, h);
+        if ((kk >> lf) == slot && (kk & (fpad - 1)) < F) prow[kk & (fpad - 1)] = sc[i];
+      }
+    }
 
-      f32x16 o[C::NT];
+    // stage this tile's 32 V rows (row index = lane row r) in the wave's LDS image
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int t = 0; t < C::NT; ++t) o[t] = zero16();
+    for (int i = 0; i < VN; ++i) {
+      const int c = h + 2 * i;
+      if (c < C::CPR) *reinterpret_cast<u32x4*>(Vs + r * C::VROW + c * C::EPC) = vv[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    f32x16 o[C::NT];
 #pragma unroll
-      for (int sp = 0; sp < M::PV_STEPS; ++sp)
+    for (int t = 0; t < C::NT; ++t) o[t] = zero16();
 #pragma unroll
-        for (int t = 0; t < C::NT; ++t) {
-          typename M::frag vf;
-          if constexpr (C::BF) vf = vt_frag_lds<C::VROW>(Vs, 0, sp, t);
-          else vf = Vs[f32_pv_key(sp, h) * C::VROW + 32 * t + r];
-          o[t] = M::mma(vf, pf[sp], o[t]);
-        }
-      if (rv) {
-        T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
+    for (int sp = 0; sp < M::PV_STEPS; ++sp)
 #pragma unroll
-        for (int t = 0; t < C::NT; ++t)
+      for (int t = 0; t < C::NT; ++t) {
+        typename M::frag vf;
+        if constexpr (C::BF) vf = vt_frag_lds<C::VROW>(Vs, 0, sp, t);
+        else vf = Vs[f32_pv_key(sp, h) * C::VROW + 32 * t + r];
+        o[t] = M::mma(vf, pf[sp], o[t]);
+      }
+    if (rv) {
+      T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
 #pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const int dc = 32 * t + 8 * gq + 4 * h;
-            if (dc < D) {
-              if constexpr (C::BF) {
-                bf16x4 v;
+      for (int t = 0; t < C::NT; ++t)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (bf16)o[t][4 * gq + j];
-                *reinterpret_cast<bf16x4*>(orow + dc) = v;
-              } else {
-                f32x4 v;
+        for (int gq = 0; gq < 4; ++gq) {
+          const int dc = 32 * t + 8 * gq + 4 * h;
+          if (dc < D) {
+            if constexpr (C::BF) {
+              bf16x4 v;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = o[t][4 * gq + j];
-                *reinterpret_cast<f32x4*>(orow + dc) = v;
-              }
+              for (int j = 0; j < 4; ++j) v[j] = (bf16)o[t][4 * gq + j];
+              *reinterpret_cast<bf16x4*>(orow + dc) = v;
+            } else {
+              f32x4 v;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = o[t][4 * gq + j];
+              *reinterpret_cast<f32x4*>(orow + dc) = v;
             }
           }
-      }
+        }
     }
   }
 }
@@ -181,7 +210,8 @@ static int launch_temporal(const vp2p_temporal_attn_args* a, hipStream_t s) {
   const int groups = p2p ? 2 : a->batch;
   const int64_t nwg = (int64_t)groups * ((a->tokens + G - 1) / G);
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-  hipLaunchKernelGGL((temporal_attn_kernel<T, D>), dim3((unsigned)nwg), dim3(256), 4 * C::WAVE_LDS, s, *a, lf);
+  hipLaunchKernelGGL((temporal_attn_p2p_kernel<T, D>), dim3((unsigned)nwg, (unsigned)((a->heads + 3) / 4)), dim3(256),
+                     4 * C::WAVE_LDS, s, *a, lf);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
