@@ -1,6 +1,7 @@
 """K7 GroupNorm (+temb add, SiLU) and K8 LayerNorm (+ residual add) at every UNet3D shape of the B4
 f8 512^2 edit, N launches each, for rocprofv3 --kernel-trace (per-launch durations by shape).
-Prints the algorithmic bytes per launch of each op/shape in launch order."""
+Prints the algorithmic bytes per launch of each op/shape in launch order.  A/B caveat as in
+tools/k2_ab.py: kernels with the same mangled name in both builds run one code object."""
 import json
 import os
 import sys
