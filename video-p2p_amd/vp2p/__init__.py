@@ -14,3 +14,4 @@ from .controllers import (AttentionControl, AttentionControlEdit, AttentionRefin
                           make_controller)
 from .attention import CrossAttention, FrameAttention, register_attention_control  # noqa
 from . import prompt_align  # noqa
+from .clip_bpe import CLIPBPETokenizer, load_tokenizer  # noqa
