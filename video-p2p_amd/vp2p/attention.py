@@ -67,9 +67,9 @@ class CrossAttention(nn.Module):
         return t.reshape(bh // h, h, n, d).permute(0, 2, 1, 3).reshape(bh // h, n, h * d)
 
     def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, video_length=None,
-                temporal_layout=None):
+                temporal_layout=None, residual=None):
         return hooked_attention(self, None, "none", hidden_states, encoder_hidden_states, attention_mask,
-                                video_length, temporal_layout)
+                                video_length, temporal_layout, residual)
 
 
 class FrameAttention(CrossAttention):
@@ -116,7 +116,7 @@ def _batch_frames(x, controller, video_length):
 
 
 def hooked_attention(module, controller, place, x, context=None, attention_mask=None, video_length=None,
-                     temporal_layout=None):
+                     temporal_layout=None, residual=None):
     """The patched forward (ptp_utils.py:196-221) for ``controller`` on the HIP kernels."""
     if attention_mask is not None:
         raise NotImplementedError("attention_mask is not supported on the fused path "
@@ -213,7 +213,30 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
         controller.fused_end(False, place, call, probs)
     if shard is not None:
         out = shard.to_frames(out, B)
-    return to_out(out)
+    return _out_proj(to_out, out, residual)
+
+
+def _out_proj(to_out, out, residual):
+    """``to_out(out)``, plus ``residual`` when the caller passes the block's residual
+    (``attn_temp(norm_temp(x)) + x``, attention.py:268).  At inference the add runs in the epilogue
+    of K10's GEMM core when that measured faster for the shape than hipBLASLt + a separate add
+    (``ops.CONV.pick``, the same per-shape choice as the proj_out fusion)."""
+    if residual is None:
+        return to_out(out)
+    if torch.is_grad_enabled() or not isinstance(to_out, nn.Linear) or not out.is_contiguous() \
+            or residual.shape[:-1] != out.shape[:-1] or residual.dtype != out.dtype:
+        return to_out(out) + residual
+    res = residual.contiguous()
+
+    def fused():
+        return ops.linear_residual(out, to_out.weight, to_out.bias, res)
+
+    def lib():
+        return to_out(out) + res
+
+    key = ("to_out_res", tuple(out.shape), tuple(to_out.weight.shape), out.device.index)
+    ok = ops.linear_residual_supported(out, to_out.weight, res)
+    return fused() if ops.CONV.pick(key, ok, fused, lib) else lib()
 
 
 def _pv(module, attn, v, B, f):
@@ -263,9 +286,10 @@ def register_attention_control(model, controller):
 
     def make_forward(net, place):
         def forward(x, encoder_hidden_states=None, attention_mask=None, video_length=None,
-                    temporal_layout=None):
+                    temporal_layout=None, residual=None):
             return hooked_attention(net, None if controller is None else ctrl, place, x,
-                                    encoder_hidden_states, attention_mask, video_length, temporal_layout)
+                                    encoder_hidden_states, attention_mask, video_length, temporal_layout,
+                                    residual)
         return forward
 
     def walk(net, count, place):
