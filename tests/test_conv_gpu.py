@@ -125,3 +125,32 @@ def test_linear_residual():
     torch.cuda.synchronize()
     err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("mode", ["k10", "library"])
+def test_attn_temp_residual_on_output_projection(mode):
+    """attn_temp(y, residual=x) (the block's last add riding on to_out, attention.py:268) equals
+    attn_temp(y) + x on either branch of the per-shape choice."""
+    from vp2p import ops
+    from vp2p.attention import CrossAttention
+    torch.manual_seed(9)
+    attn = CrossAttention(320, heads=8, dim_head=40).to(DEV, torch.bfloat16)
+    with torch.no_grad():
+        attn.to_out[0].weight.normal_(0, 0.05)
+        attn.to_out[0].bias.normal_(0, 0.1)
+    f = 8
+    y = torch.randn(2 * f, 256, 320, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(2 * f, 256, 320, device=DEV, dtype=torch.bfloat16)
+    saved_mode, saved_choice = ops.CONV.mode, dict(ops.CONV.choice)
+    ops.CONV.mode, ops.CONV.choice = mode, {}
+    try:
+        with torch.no_grad():
+            ref = (attn(y, video_length=f, temporal_layout="bf") + x).float()
+            out = attn(y, video_length=f, temporal_layout="bf", residual=x).float()
+        torch.cuda.synchronize()
+    finally:
+        ops.CONV.mode, ops.CONV.choice = saved_mode, saved_choice
+    err = (out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
+    if mode == "library":
+        assert torch.equal(out, ref)
