@@ -21,6 +21,22 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_models():
+    """Reference outputs of tuneavideo's own model files (tests/golden/make_golden_models.py)."""
+    import numpy as np
+    return np.load(os.path.join(ROOT, "tests", "golden", "golden_models.npz"))
+
+
+def model_state(module_factory, seed: int):
+    """{name: fp32 CPU tensor} of ``module_factory()``'s state dict filled by model_spec.param_values
+    (the weights make_golden_models.py gave the reference's module of the same keys)."""
+    import torch
+    import model_spec as MS
+    keys = {k: tuple(v.shape) for k, v in module_factory().state_dict().items()}
+    return {k: torch.from_numpy(MS.param_values(k, s, seed)) for k, s in keys.items()}
+
+
+@pytest.fixture(scope="session")
 def tokenizer():
     from vp2p.tokenizer import SyntheticCLIPTokenizer
     return SyntheticCLIPTokenizer()

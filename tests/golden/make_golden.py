@@ -169,9 +169,32 @@ class MiniUNet(nn.Module):
                      ("up_blocks", self.up_blocks)])
 
 
+def guard_finite(ns) -> List[str]:
+    """Record every controller call whose input probabilities are not finite.
+
+    The reference hook's global-max softmax (ptp_utils.py:217) underflows to 0/0 for rows whose
+    maximum sits ~88 below the tensor's maximum; such a layer would pin nothing (a row-max kernel
+    is finite there), so EVERY hooked call of the golden sequence -- saved or not -- must be finite.
+    The check wraps ``AttentionControl.__call__`` (run_videop2p.py:212-224), the one place every
+    hooked probability tensor passes through."""
+    bad: List[str] = []
+    cls = ns["AttentionControl"]
+    orig = cls.__call__
+
+    def checked(self, attn, is_cross, place_in_unet):
+        if not torch.isfinite(attn).all():
+            bad.append(f"step {self.cur_step} layer {self.cur_att_layer} ({place_in_unet}, "
+                       f"{'cross' if is_cross else 'self'}): {int((~torch.isfinite(attn)).sum())} non-finite")
+        return orig(self, attn, is_cross, place_in_unet)
+
+    cls.__call__ = checked
+    return bad
+
+
 def main():
     tok = SyntheticCLIPTokenizer()
     ref_seq, ptp, ns, make_scheduler = load_reference(tok)
+    nonfinite_calls = guard_finite(ns)
     out: Dict[str, np.ndarray] = {}
 
     # ---- host logic: mappers, word indices, alphas, equalizers -------------------------------
@@ -268,6 +291,8 @@ def main():
         out[f"ddim/next_step/{t}"] = inv.next_step(eps, t, x).numpy()
         out[f"ddim/prev_step/{t}"] = inv.prev_step(eps, t, x).numpy()
 
+    if nonfinite_calls:
+        raise RuntimeError(f"{len(nonfinite_calls)} hooked calls left the finite regime: {nonfinite_calls[:5]}")
     bad = [k for k, v in out.items() if v.dtype.kind == "f" and not np.isfinite(v).all()]
     if bad:  # the reference's global-max softmax underflows (ptp_utils.py:217): keep inputs finite
         raise RuntimeError(f"non-finite reference outputs: {bad[:5]}")

@@ -1,0 +1,119 @@
+"""Seeded definition of the MODEL-level golden fixtures (``golden_models.npz``, ``golden_edit_*.npz``).
+
+``make_golden_models.py`` (build container only) runs the reference's own tuneavideo model files
+and TuneAVideoPipeline loop on these inputs; the tests regenerate the same inputs and weights from
+this module, so the committed fixtures hold only reference OUTPUTS.
+
+Weights: ``fill_`` draws every state-dict entry from its own numpy PCG64 stream keyed by
+(seed, crc32(name)), so the values depend only on the parameter's name and shape -- the
+reference's modules and vp2p's (same state-dict keys) receive identical weights whatever order
+their constructors register them in.  The SD-1.5-geometry edit fixtures use
+``vp2p.unet3d.init_random_`` instead (the bench's weights; torch's CPU generator, identical on
+this image and the GPU box).
+"""
+from __future__ import annotations
+
+import zlib
+from typing import Dict
+
+import numpy as np
+
+HEADS = 8
+
+# FrameAttention (attention.py:273-329): name -> (batch, frames, tokens, channels); head dim = C/8
+FA_CONFIGS = {"d40": (2, 3, 80, 320), "d80": (1, 4, 64, 640), "d160": (2, 2, 48, 1280)}
+# Transformer3DModel (attention.py:32-137): name -> (batch, frames, h, w, channels, cross_dim)
+T3D_CONFIGS = {"c320": (2, 3, 8, 8, 320, 768), "c640": (2, 2, 4, 6, 640, 768)}
+# ResnetBlock3D (resnet.py:111-205): name -> (batch, frames, h, w, cin, cout, temb)
+RN_CONFIGS = {"c320_640": (2, 3, 8, 8, 320, 640, 1280), "c640": (2, 2, 4, 4, 640, 640, 1280)}
+# Whole UNet3DConditionModel at the SD-1.5 geometry (unet.py:42-79 defaults, cross dim 768) on a
+# small latent: (batch, frames, latent h, latent w)
+UNET_SMALL = (2, 2, 16, 16)
+UNET_SMALL_T = 501
+UNET_EDIT_STEPS = (0, 45)          # controller cur_step of the two controlled forwards (bird edit)
+
+# End-to-end edits through the reference pipeline loop (pipeline_tuneavideo.py:394-430):
+# name -> (edit, frames, steps run of the 50-step schedule, steps whose latents are saved)
+EDITS = {
+    "car2": ("car", 2, 12, (0, 9, 10, 11)),
+    "rabbit8": ("rabbit", 8, 50, (0, 10, 11, 24, 25, 49)),
+    "penguin24": ("penguin", 24, 12, (10, 11)),
+}
+
+
+def rng(*key: int) -> np.random.Generator:
+    return np.random.default_rng(np.random.SeedSequence(list(key)))
+
+
+def param_values(name: str, shape, seed: int) -> np.ndarray:
+    """Deterministic value of one state-dict entry.  Weights ~ N(0, 1/fan_in) (unit-gain
+    projections, so activations neither vanish nor blow up through the blocks), biases ~ N(0, 0.1^2),
+    norm scales ~ 1 + N(0, 0.1^2), norm shifts ~ N(0, 0.1^2)."""
+    g = rng(seed, zlib.crc32(name.encode()))
+    shape = tuple(shape)
+    leaf = name.rsplit(".", 1)[-1]
+    is_norm = "norm" in name.rsplit(".", 2)[-2] if name.count(".") >= 1 else False
+    if leaf == "weight" and is_norm:
+        v = 1.0 + 0.1 * g.standard_normal(shape)
+    elif leaf == "bias":
+        v = 0.1 * g.standard_normal(shape)
+    else:
+        fan_in = int(np.prod(shape[1:])) if len(shape) > 1 else 1
+        v = g.standard_normal(shape) / np.sqrt(fan_in)
+    return v.astype(np.float32)
+
+
+def fill_(module, seed: int):
+    """Overwrite every parameter of ``module`` (a torch nn.Module) with ``param_values``."""
+    import torch
+    with torch.no_grad():
+        for name, p in module.state_dict().items():
+            if p.dtype.is_floating_point:
+                p.copy_(torch.from_numpy(param_values(name, p.shape, seed)))
+    return module
+
+
+def fa_input(name: str) -> np.ndarray:
+    B, f, N, C = FA_CONFIGS[name]
+    return rng(31, zlib.crc32(name.encode())).standard_normal((B * f, N, C)).astype(np.float32)
+
+
+def t3d_inputs(name: str):
+    """(hidden (B, C, f, h, w), context (B, 77, D))."""
+    B, f, h, w, C, D = T3D_CONFIGS[name]
+    g = rng(32, zlib.crc32(name.encode()))
+    return (g.standard_normal((B, C, f, h, w)).astype(np.float32),
+            g.standard_normal((B, 77, D)).astype(np.float32))
+
+
+def rn_inputs(name: str):
+    """(hidden (B, Cin, f, h, w), temb (B, T))."""
+    B, f, h, w, cin, cout, T = RN_CONFIGS[name]
+    g = rng(33, zlib.crc32(name.encode()))
+    return g.standard_normal((B, cin, f, h, w)).astype(np.float32), g.standard_normal((B, T)).astype(np.float32)
+
+
+def unet_small_inputs(batch: int = None):
+    """(sample (B, 4, f, h, w), context (B, 77, 768)); ``batch`` overrides B (4 for the edit forwards:
+    rows [uncond x 2, cond x 2] with identical uncond rows)."""
+    B, f, h, w = UNET_SMALL
+    B = batch or B
+    g = rng(34, B)
+    sample = g.standard_normal((B, 4, f, h, w)).astype(np.float32)
+    ctx = g.standard_normal((B, 77, 768)).astype(np.float32)
+    if B == 4:
+        sample[1] = sample[0]
+        sample[3] = sample[2]
+        ctx[1] = ctx[0]
+    return sample, ctx
+
+
+def edit_inputs(name: str) -> Dict[str, np.ndarray]:
+    """x_T (1, 4, f, 64, 64) and the CFG text embeddings [uncond, uncond, cond_0, cond_1] (4, 77, 768)
+    of one end-to-end edit."""
+    _, f, _, _ = EDITS[name]
+    g = rng(35, zlib.crc32(name.encode()))
+    x_t = g.standard_normal((1, 4, f, 64, 64)).astype(np.float32)
+    unc = g.standard_normal((1, 77, 768)).astype(np.float32)
+    cond = g.standard_normal((2, 77, 768)).astype(np.float32)
+    return {"x_t": x_t, "emb": np.concatenate([unc, unc, cond]).astype(np.float32)}

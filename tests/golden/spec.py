@@ -62,8 +62,8 @@ def block_weights(cfg_id: int, block: int):
     for li, (name, ctx) in enumerate((("attn2", CTX), ("attn_temp", C))):
         g = rng(11, cfg_id, block, li)
         out[name] = {
-            "to_q": (g.standard_normal((C, C)) * 0.35).astype(np.float32),
-            "to_k": (g.standard_normal((C, ctx)) * 0.35).astype(np.float32),
+            "to_q": (g.standard_normal((C, C)) * 0.25).astype(np.float32),
+            "to_k": (g.standard_normal((C, ctx)) * 0.25).astype(np.float32),
             "to_v": (g.standard_normal((C, ctx)) * 0.5).astype(np.float32),
             "to_out_w": (g.standard_normal((C, C)) * 0.4).astype(np.float32),
             "to_out_b": (g.standard_normal((C,)) * 0.1).astype(np.float32),
@@ -77,7 +77,7 @@ def text_embeddings(cfg_id: int) -> np.ndarray:
     unc = g.standard_normal((1, WORDS, CTX)).astype(np.float32)
     cond = g.standard_normal((P, WORDS, CTX)).astype(np.float32)
     for p, tok in enumerate(BLEND_TOKEN[SEQ_CONFIGS[cfg_id]]):
-        cond[p, tok] *= 4.0   # the blend word dominates the disk queries (see block_inputs)
+        cond[p, tok] *= 2.5   # the blend word dominates the disk queries (see block_inputs)
     return np.concatenate([np.repeat(unc, P, axis=0), cond], axis=0)
 
 
