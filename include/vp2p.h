@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 6
+#define VP2P_ABI_VERSION 7
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -113,16 +113,19 @@ typedef struct vp2p_cross_attn_args {
   const float* map_val;     /* REPLACE: value of each nonzero */
   const float* refine_alpha;/* REFINE: (prompts-1, tokens_kv) */
   const float* equalizer;   /* (tokens_kv) */
-  /* AttentionStore sum consumed by LocalBlend: lb_acc[p][frame][token] += sum over heads and words
-   * of lb_word_alpha[p][w] * post-edit prob (conditional rows only).  NULL = off. */
-  float* lb_acc;            /* (prompts, frames, tokens_q) fp32 */
-  const float* lb_word_alpha; /* (prompts, tokens_kv) */
+  /* AttentionStore sum consumed by LocalBlend: lb_acc[s][p][frame][token] += sum over heads and words
+   * of lb_word_alpha[s][p][w] * post-edit prob (conditional rows only).  NULL = off.  Set s = 0 holds
+   * the blend words (alpha_layers), set 1 -- when lb_sets = 2 -- LocalBlend's substruct_words
+   * (substruct_layers, run_videop2p.py:149-151, 166-174). */
+  float* lb_acc;            /* (lb_sets, prompts, frames, tokens_q) fp32 */
+  const float* lb_word_alpha; /* (lb_sets, prompts, tokens_kv) */
   /* Optional post-edit probabilities in the reference's attn layout
    * ((batch*frames*heads), tokens_q, tokens_kv) fp32.  NULL = off. */
   float* probs_out;
-  /* Scratch for the per-head LocalBlend partials, (prompts, heads, frames*tokens_q) fp32; required
-   * when lb_acc is set (the head sum is finished in a fixed order by a second pass). */
+  /* Scratch for the per-head LocalBlend partials, (lb_sets, prompts, heads, frames*tokens_q) fp32;
+   * required when lb_acc is set (the head sum is finished in a fixed order by a second pass). */
   float* lb_ws;
+  int32_t lb_sets;          /* word-weight sets accumulated: 1 (0 is read as 1) or 2 */
 } vp2p_cross_attn_args;
 
 /* Bytes of the K/V workspace for one context of the given shape (<0: unsupported). */
@@ -178,8 +181,9 @@ int vp2p_temporal_attn_bwd(const vp2p_temporal_attn_bwd_args* args, void* stream
 /* ---- K5+K6: classifier-free guidance + DDIM update + LocalBlend, one launch --------------------
  *   e_p   = cfg ? u_p + g*(t_p - u_p) : n_p        (fast: e_0 = t_0)
  *   x'_p  = c4 * ((x_p - c1*e_p) / c2) + c3*e_p    (each op rounded separately, as torch does)
- *   blend : x''_p = x'_0 + m_p*(x'_p - x'_0), m_p = mask_0 | mask_p,
- *           mask_p = up(pool3x3(lb_acc_p / lb_count)) / max(...) > th                           */
+ *   blend : x''_p = x'_0 + m_p*(x'_p - x'_0), m_p = (mask_0 | mask_p) & ~(sub_0 | sub_p),
+ *           mask_p = up(pool3x3(lb_acc_p / lb_count)) / max(...) > th
+ *           sub_p  = up(lb_sub_p / lb_count) / max(...) > sub_th   (no pool; only when lb_sub)    */
 typedef struct vp2p_step_args {
   const void* noise;        /* (cfg ? 2*prompts : prompts, channels, frames, height, width) contiguous */
   int32_t noise_dtype;
@@ -193,6 +197,8 @@ typedef struct vp2p_step_args {
   int32_t lb_h, lb_w;
   float lb_count;           /* number of maps summed per step (layers*heads): the reference's mean */
   float lb_th;
+  const float* lb_sub;      /* (prompts, frames, lb_h*lb_w) substruct_words sum, or NULL (run_videop2p.py:149-151) */
+  float lb_sub_th;          /* th[1] */
 } vp2p_step_args;
 
 int vp2p_step_fused(const vp2p_step_args* args, void* stream);

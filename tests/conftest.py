@@ -20,6 +20,16 @@ def golden():
     return np.load(os.path.join(ROOT, "tests", "golden", "golden.npz"))
 
 
+def record(test: str, **metrics):
+    """Append measured parity numbers to $VP2P_PARITY_REPORT (JSON lines) when it is set, so a GPU
+    run leaves the actual errors / PSNRs behind (profiles/r02_parity_*.jsonl)."""
+    path = os.environ.get("VP2P_PARITY_REPORT")
+    if path:
+        import json
+        with open(path, "a") as fh:
+            fh.write(json.dumps({"test": test, **metrics}) + "\n")
+
+
 @pytest.fixture(scope="session")
 def golden_models():
     """Reference outputs of tuneavideo's own model files (tests/golden/make_golden_models.py)."""

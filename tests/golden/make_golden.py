@@ -269,6 +269,11 @@ def main():
                 maps = torch.cat(maps, dim=2)
                 out[f"seq/{name}/lbmask/{step}"] = lb.get_mask(maps, lb.alpha_layers, True).numpy()
                 out[f"seq/{name}/lbmaps/{step}"] = (maps * lb.alpha_layers).sum(-1).mean(2).numpy()
+                # the same store through a LocalBlend with substruct_words (mask & ~substruct mask)
+                sw = spec.SUBSTRUCT[name]
+                lbs = ns["LocalBlend"](prompts, ns["blend_word"], substruct_words=((sw,), (sw,)))
+                lbs.counter = lbs.start_blend
+                out[f"seq/{name}/lbsub/{step}"] = lbs(lat.clone(), ctrl.attention_store, step).numpy()
         out[f"seq/{name}/final_step"] = np.array(ctrl.cur_step)
         out[f"seq/{name}/lb_counter"] = np.array(ctrl.local_blend.counter)
         out[f"seq/{name}/store_len_down_cross"] = np.array(len(ctrl.attention_store["down_cross"]))

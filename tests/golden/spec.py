@@ -50,6 +50,8 @@ CONFIGS = {
 }
 SEQ_CONFIGS = ("rabbit", "car")   # configs driven through the mini-UNet step sequence
 BLEND_TOKEN = {"rabbit": (2, 3), "car": (7, 7)}   # token index of blend_word[p] in prompt p
+# LocalBlend(substruct_words=...) probe (run_videop2p.py:149-151, 166-174): a word in both prompts
+SUBSTRUCT = {"rabbit": "grass", "car": "car"}
 
 
 def rng(*key: int) -> np.random.Generator:

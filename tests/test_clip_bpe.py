@@ -112,5 +112,7 @@ def test_multi_token_words_and_host_logic_agree(toks):
 def test_load_tokenizer_picks_files(toks, tmp_path):
     _, _, d = toks
     assert isinstance(load_tokenizer(str(d), subfolder=None), CLIPBPETokenizer)
-    assert isinstance(load_tokenizer(str(tmp_path)), SyntheticCLIPTokenizer)
+    with pytest.raises(FileNotFoundError):        # a path without the files is an error, not a fallback
+        load_tokenizer(str(tmp_path))
     assert isinstance(load_tokenizer(None), SyntheticCLIPTokenizer)
+    assert isinstance(load_tokenizer(str(tmp_path), synthetic=True), SyntheticCLIPTokenizer)

@@ -209,7 +209,8 @@ def test_temporal_attention_p2p(tokenizer, dtype, frames, d, step):
 
 
 # ------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("t,fast,blend", [(981, True, True), (501, False, True), (21, True, False)])
+@pytest.mark.parametrize("t,fast,blend", [(981, True, True), (501, False, True), (21, True, False),
+                                          (501, True, "substruct")])
 def test_step_fused(t, fast, blend):
     from vp2p import ops
     P, C, F, H, W = 2, 4, 3, 64, 64
@@ -217,14 +218,19 @@ def test_step_fused(t, fast, blend):
     noise = g.standard_normal((2 * P, C, F, H, W)).astype(np.float32)
     lat = g.standard_normal((P, C, F, H, W)).astype(np.float32)
     acc = np.abs(g.standard_normal((P, F, 256))).astype(np.float32) * 5
+    if blend == "substruct":     # (sets, P, F, 256): blend words, substruct words (th[1] = 0.5, no pool)
+        acc = np.stack([acc, np.abs(g.standard_normal((P, F, 256))).astype(np.float32) * 5])
     d = O.DDIM()
     d.set_timesteps(50)
     eps = O.cfg(noise, 7.5, fast)
     prev = d.step(eps, t, lat)
     if blend:
         lb = O.LocalBlend.__new__(O.LocalBlend)
-        lb.th, lb.latent_hw = (0.3, 0.3), (H, W)
-        mask = lb.mask_from_word_maps((acc / np.float32(40)).reshape(P, F, 16, 16), True)
+        lb.th, lb.latent_hw = (0.3, 0.5), (H, W)
+        a0 = acc[0] if blend == "substruct" else acc
+        mask = lb.mask_from_word_maps((a0 / np.float32(40)).reshape(P, F, 16, 16), True)
+        if blend == "substruct":
+            mask = mask & ~lb.mask_from_word_maps((acc[1] / np.float32(40)).reshape(P, F, 16, 16), False)
         ref = O.blend_latents(prev, mask)
     else:
         ref = prev
@@ -233,7 +239,8 @@ def test_step_fused(t, fast, blend):
     a_p = d.alphas_cumprod[prev_t] if prev_t >= 0 else d.final_alpha_cumprod
     consts = (np.sqrt(np.float32(1) - a_t), np.sqrt(a_t), np.sqrt(np.float32(1) - a_p - np.float32(0)), np.sqrt(a_p))
     out = ops.step_fused(torch.from_numpy(noise).to(DEV), torch.from_numpy(lat).to(DEV), consts, 7.5, True, fast,
-                         lb_acc=torch.from_numpy(acc).to(DEV) if blend else None, lb_count=40.0, lb_th=0.3)
+                         lb_acc=torch.from_numpy(acc).to(DEV) if blend else None, lb_count=40.0, lb_th=0.3,
+                         lb_sub_th=0.5)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
 

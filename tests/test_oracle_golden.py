@@ -92,6 +92,11 @@ def test_step_sequence(golden, tokenizer, cfg_id, name):
             flips += int((mask != ref_mask).sum())
             same = np.broadcast_to((mask == ref_mask)[:, None], res.shape)
             np.testing.assert_array_equal(res[same], golden[f"seq/{name}/lb/{step}"][same])
+            # LocalBlend(substruct_words=...): blend mask & ~(no-pool substruct mask) (run_videop2p.py:149-151)
+            sw = spec.SUBSTRUCT[name]
+            lbs = O.LocalBlend(prompts, ((blend[0],), (blend[1],)), tokenizer, substruct_words=((sw,), (sw,)))
+            lbs.counter = lbs.start_blend
+            np.testing.assert_array_equal(lbs(lat.copy(), ctrl.attention_store), golden[f"seq/{name}/lbsub/{step}"])
     assert flips == 0
     assert ctrl.cur_step == int(golden[f"seq/{name}/final_step"])
     assert ctrl.local_blend.counter == int(golden[f"seq/{name}/lb_counter"])

@@ -63,15 +63,26 @@ def test_unet_forward_matches_oracle(tokenizer, dtype, tol, name, step):
     maps = np.concatenate([m.reshape(P, -1, 8, 16, 16, 77) for m in maps], axis=2)
     lb = octrl.local_blend
     ref_lb = (maps * lb.alpha_layers).sum(-1).sum(2).reshape(P, F_, 256)
-    got_lb = ctrl.attention_store.lb_acc.cpu().numpy()
+    got_lb = ctrl.attention_store.lb_acc.cpu().numpy()     # (P, f, 256): one word set
     assert np.abs(got_lb - ref_lb).max() / np.abs(ref_lb).max() < tol
 
 
-def test_edit_loop_fast_mode(tokenizer):
+@pytest.mark.parametrize("substruct", [None, "grass"])
+def test_edit_loop_fast_mode(tokenizer, substruct):
     """Three denoising steps through the pipeline (fused CFG + DDIM + LocalBlend) vs the oracle,
-    with LocalBlend forced on from the first step (start_blend = 0)."""
+    with LocalBlend forced on from the first step (start_blend = 0); optionally with
+    LocalBlend(substruct_words=...) (run_videop2p.py:149-151: a second word-weighted sum accumulated
+    by K2, thresholded without pooling by K6)."""
+    from vp2p.controllers import LocalBlend
     from vp2p.pipeline import VideoP2PPipeline
     unet, sd, ctrl, octrl = _setup(tokenizer, "rabbit", torch.float32, seed=3)
+    if substruct:
+        prompts = spec.CONFIGS["rabbit"][0]
+        sub = ((substruct,), (substruct,))
+        ctrl.local_blend = LocalBlend(prompts, (("rabbit",), ("rabbit",)), tokenizer, substruct_words=sub)
+        ctrl._plan = None
+        octrl.local_blend.substruct_layers = O.LocalBlend._layers(prompts, sub, tokenizer)
+        assert ctrl.local_blend.sets == 2
     ctrl.local_blend.start_blend = 0
     octrl.local_blend.start_blend = 0
     x, ctx = _inputs(5)

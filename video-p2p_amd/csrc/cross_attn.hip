@@ -129,8 +129,9 @@ void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
       etab[i] = t;
     }
   }
+  const int LBS = a.lb_sets == 2 ? 2 : 1;     // word-weight sets: blend words (+ substruct words)
   if (lb)
-    for (int i = tid; i < RP * NKV; i += 256) lbw[i] = a.lb_word_alpha[i];
+    for (int i = tid; i < LBS * RP * NKV; i += 256) lbw[i] = a.lb_word_alpha[i];
   if (edit || lb) __syncthreads();
 
   const float cs = a.scale * kLog2e;
@@ -251,17 +252,20 @@ void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
           }
       }
     }
-    if (lb) {  // this head's word-weighted map of token qi -> lb_ws[p][head][qi]
-      float part = 0.f;
+    if (lb) {  // this head's word-weighted map of token qi -> lb_ws[set][p][head][qi]
+      for (int set = 0; set < LBS; ++set) {
+        const float* wts = lbw + (set * RP + p) * NKV;
+        float part = 0.f;
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int wd = kb * 32 + acc_row(i, h);
-          if (wd < NKV) part += lbw[p * NKV + wd] * sc[kb][i];
-        }
-      part += xhalf(part);
-      if (h == 0 && qv) a.lb_ws[((int64_t)p * a.heads + head) * FQ + qi] = part;
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) part += wts[wd] * sc[kb][i];
+          }
+        part += xhalf(part);
+        if (h == 0 && qv) a.lb_ws[((int64_t)(set * RP + p) * a.heads + head) * FQ + qi] = part;
+      }
     }
     if (a.probs_out && qv) {
       float* prow_out = a.probs_out + ((((int64_t)b * a.frames + fr) * a.heads + head) * a.tokens_q + pos) * NKV;
@@ -365,16 +369,17 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
   const int64_t nwg = std::min<int64_t>(items, 0x7fffffff);
   const int prow = a->tokens_kv | 1;           // odd fp32 row stride: conflict-free per-lane rows
   const int rp = p2p ? a->prompts : 1;
+  const int sets = a->lb_sets == 2 ? 2 : 1;
   const size_t lds = (size_t)4 * 32 * prow * sizeof(float) + (size_t)(rp - 1) * a->tokens_kv * 16 +
-                     (size_t)rp * a->tokens_kv * sizeof(float);
+                     (size_t)sets * rp * a->tokens_kv * sizeof(float);
   hipLaunchKernelGGL((cross_attn_kernel<T, D, KB>), dim3((unsigned)nwg, (unsigned)groups), dim3(256), lds, s,
                      *a, prow);
   if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
-  if (p2p && a->lb_acc) {
-    const int64_t n = (int64_t)a->prompts * FQ;
+  if (p2p && a->lb_acc) {   // (set, prompt) pairs are contiguous: reduce them as sets*prompts rows
+    const int64_t n = (int64_t)sets * a->prompts * FQ;
     const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(cross_lb_reduce_kernel, dim3(blocks), dim3(256), 0, s, a->lb_acc, a->lb_ws,
-                       a->prompts, a->heads, FQ);
+                       sets * a->prompts, a->heads, FQ);
     if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
   }
   return VP2P_OK;
@@ -463,6 +468,7 @@ extern "C" int vp2p_cross_attn_p2p_fwd(const vp2p_cross_attn_args* a, void* stre
     if (a->reweight && !a->equalizer) return VP2P_E_ARG;
   }
   if (a->lb_acc && (!p2p || !a->lb_word_alpha || !a->lb_ws)) return VP2P_E_ARG;
+  if (a->lb_sets < 0 || a->lb_sets > 2) return VP2P_E_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
 #define VP2P_CROSS(DIM) \
   case DIM: return a->dtype == VP2P_BF16 ? launch_cross_kb<bf16, DIM>(a, s) : launch_cross_kb<float, DIM>(a, s);

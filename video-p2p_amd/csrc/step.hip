@@ -26,6 +26,7 @@ __global__ __launch_bounds__(256) void step_kernel(const vp2p_step_args a) {
 #pragma clang fp contract(off)
   __shared__ float pooled[kMaxPrompts * kMaxLbPix];
   __shared__ float pmax[kMaxPrompts];
+  __shared__ float submax[kMaxPrompts];
   const int P = a.prompts, Cc = a.channels, F = a.frames, H = a.height, W = a.width;
   const int fr = blockIdx.x % F, c = blockIdx.x / F;
   const bool lb = a.lb_acc != nullptr;
@@ -47,13 +48,27 @@ __global__ __launch_bounds__(256) void step_kernel(const vp2p_step_args a) {
     __syncthreads();
     const int wv = tid >> 6, ln = tid & 63;
     for (int p = wv; p < P; p += blockDim.x >> 6) {
-      float m = kNegInf;
-      for (int k = ln; k < LHW; k += 64) m = fmaxf(m, pooled[p * kMaxLbPix + k]);
-      for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-      if (ln == 0) pmax[p] = m;
+      float m = kNegInf, ms = kNegInf;
+      for (int k = ln; k < LHW; k += 64) {
+        m = fmaxf(m, pooled[p * kMaxLbPix + k]);
+        if (a.lb_sub) ms = fmaxf(ms, a.lb_sub[((int64_t)p * F + fr) * LHW + k] / a.lb_count);
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        m = fmaxf(m, __shfl_xor(m, off));
+        ms = fmaxf(ms, __shfl_xor(ms, off));
+      }
+      if (ln == 0) {
+        pmax[p] = m;
+        submax[p] = ms;
+      }
     }
     __syncthreads();
   }
+  // substruct_words mask (run_videop2p.py:149-151): get_mask(maps, substruct_layers, use_pool=False),
+  // i.e. no pooling and threshold th[1]; it removes pixels from the blend mask
+  auto sub_at = [&](int p, int k) {
+    return a.lb_sub[((int64_t)p * F + fr) * LHW + k] / a.lb_count / submax[p] > a.lb_sub_th;
+  };
 
   const float sy_scale = (float)LH / (float)H, sx_scale = (float)LW / (float)W;
   const int64_t HW = (int64_t)H * W;
@@ -79,8 +94,10 @@ __global__ __launch_bounds__(256) void step_kernel(const vp2p_step_args a) {
       const int sx = min((int)floorf((float)x * sx_scale), LW - 1);
       const int k = sy * LW + sx;
       const bool m0 = pooled[k] / pmax[0] > a.lb_th;
+      const bool s0 = a.lb_sub && sub_at(0, k);
       for (int p = 0; p < P; ++p) {
-        const bool mp = m0 || (pooled[p * kMaxLbPix + k] / pmax[p] > a.lb_th);
+        bool mp = m0 || (pooled[p * kMaxLbPix + k] / pmax[p] > a.lb_th);
+        if (a.lb_sub) mp = mp && !(s0 || sub_at(p, k));
         const float mf = mp ? 1.f : 0.f;
         a.out[(((int64_t)p * Cc + c) * F + fr) * HW + e] = prev[0] + mf * (prev[p] - prev[0]);
       }

@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
@@ -89,7 +89,7 @@ class CrossAttnArgs(ctypes.Structure):
                 ("alpha_words", c_void_p), ("map_ptr", c_void_p), ("map_idx", c_void_p),
                 ("map_val", c_void_p), ("refine_alpha", c_void_p), ("equalizer", c_void_p),
                 ("lb_acc", c_void_p), ("lb_word_alpha", c_void_p), ("probs_out", c_void_p),
-                ("lb_ws", c_void_p)]
+                ("lb_ws", c_void_p), ("lb_sets", c_int32)]
 
 
 class TemporalAttnArgs(ctypes.Structure):
@@ -109,7 +109,7 @@ class StepArgs(ctypes.Structure):
                 ("width", c_int32), ("cfg", c_int32), ("fast", c_int32), ("guidance", c_float),
                 ("c1", c_float), ("c2", c_float), ("c3", c_float), ("c4", c_float),
                 ("lb_acc", c_void_p), ("lb_h", c_int32), ("lb_w", c_int32), ("lb_count", c_float),
-                ("lb_th", c_float)]
+                ("lb_th", c_float), ("lb_sub", c_void_p), ("lb_sub_th", c_float)]
 
 
 class NullTextLossArgs(ctypes.Structure):

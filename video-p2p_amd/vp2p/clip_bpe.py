@@ -19,12 +19,13 @@ tokenizer directory gives the reference's token ids without a network or ``trans
 
 ``decode`` joins the token strings, maps back to bytes and turns ``</w>`` into a space, so
 ``decode([id]).strip()`` is the piece text ``get_word_inds`` accumulates (ptp_utils.py:266-272).
-``load_tokenizer`` picks this tokenizer when the files exist and the offline synthetic one
-otherwise.
+``load_tokenizer`` loads this tokenizer from a directory (raising if the files are missing) and
+returns the offline synthetic one only when asked for explicitly.
 """
 from __future__ import annotations
 
 import json
+import logging
 import os
 from functools import lru_cache
 from typing import Dict, List, Optional, Sequence, Tuple, Union
@@ -33,6 +34,8 @@ import regex
 import torch
 
 from .tokenizer import SyntheticCLIPTokenizer, _Encoding
+
+log = logging.getLogger("vp2p")
 
 BOS = "<|startoftext|>"
 EOS = "<|endoftext|>"
@@ -165,11 +168,21 @@ class CLIPBPETokenizer:
         return _Encoding(ids, mask)
 
 
-def load_tokenizer(path: Optional[str] = None, subfolder: Optional[str] = "tokenizer"):
-    """Real CLIP BPE from ``<path>/<subfolder>/{vocab.json,merges.txt}`` when present, else the
-    offline synthetic tokenizer (run_videop2p.py:101 loads the former)."""
-    if path:
-        for d in ((os.path.join(path, subfolder) if subfolder else path), path):
-            if os.path.isfile(os.path.join(d, "vocab.json")) and os.path.isfile(os.path.join(d, "merges.txt")):
-                return CLIPBPETokenizer.from_pretrained(d)
-    return SyntheticCLIPTokenizer()
+def load_tokenizer(path: Optional[str] = None, subfolder: Optional[str] = "tokenizer", synthetic: bool = False):
+    """The real CLIP BPE from ``<path>/<subfolder>/{vocab.json,merges.txt}`` (run_videop2p.py:101).
+
+    The offline synthetic tokenizer is returned only when asked for explicitly (``path=None`` or
+    ``synthetic=True``): a path whose vocabulary files are missing raises ``FileNotFoundError``
+    instead of silently tokenising with made-up ids (which would give every mapper, word index
+    and LocalBlend layer a tokenisation different from CLIP's)."""
+    if synthetic or not path:
+        log.info("vp2p: using the synthetic CLIP tokenizer (no vocabulary files)")
+        return SyntheticCLIPTokenizer()
+    tried = []
+    for d in ((os.path.join(path, subfolder) if subfolder else path), path):
+        tried.append(d)
+        if os.path.isfile(os.path.join(d, "vocab.json")) and os.path.isfile(os.path.join(d, "merges.txt")):
+            log.info("vp2p: CLIP BPE tokenizer from %s", d)
+            return CLIPBPETokenizer.from_pretrained(d)
+    raise FileNotFoundError(f"no CLIP vocab.json + merges.txt under {tried}; pass synthetic=True for the offline "
+                            "synthetic tokenizer")

@@ -74,7 +74,7 @@ class LocalBlend:
             raise ValueError("LocalBlend needs the tokenizer (the reference closes over main's)")
         self.alpha_layers = self._layers(prompts, words, tokenizer)
         self.substruct_layers = None
-        if substruct_words is not None:
+        if substruct_words is not None:      # run_videop2p.py:166-174
             self.substruct_layers = self._layers(prompts, substruct_words, tokenizer)
         self.start_blend = int(start_blend * num_steps)
         self.counter = 0
@@ -89,15 +89,23 @@ class LocalBlend:
         return a
 
     def word_alpha(self) -> torch.Tensor:
-        return self.alpha_layers.reshape(self.alpha_layers.shape[0], MAX_NUM_WORDS)
+        """Word weights the cross kernel accumulates with: (P, 77), or (2, P, 77) when
+        ``substruct_words`` is set (set 1 feeds the substruct mask, run_videop2p.py:149-151)."""
+        P = self.alpha_layers.shape[0]
+        a = self.alpha_layers.reshape(P, MAX_NUM_WORDS)
+        if self.substruct_layers is None:
+            return a
+        return torch.stack([a, self.substruct_layers.reshape(P, MAX_NUM_WORDS)])
+
+    @property
+    def sets(self) -> int:
+        return 1 if self.substruct_layers is None else 2
 
     def advance(self, attention_store: AttentionMaps) -> Optional[torch.Tensor]:
         """Count this step's callback (:143-144); return the LocalBlend sum if the blend fires."""
         self.counter += 1
         if self.counter <= self.start_blend:
             return None
-        if self.substruct_layers is not None:
-            raise NotImplementedError("LocalBlend(substruct_words=...) is not on the fused path")
         if attention_store.lb_acc is None:
             raise ValueError("LocalBlend has no res-16 cross-attention maps to blend with "
                              "(the reference reshapes them to 8 heads x 16 x 16, run_videop2p.py:146)")
@@ -113,7 +121,8 @@ class LocalBlend:
         # identity DDIM constants: the fused step kernel then only applies the blend
         zeros = torch.zeros_like(x)
         return ops.step_fused(zeros, x, (0.0, 1.0, 0.0, 1.0), cfg=False, lb_acc=acc, lb_hw=LB_HW,
-                              lb_count=float(attention_store.lb_layers_per_step * 8), lb_th=self.th[0])
+                              lb_count=float(attention_store.lb_layers_per_step * 8), lb_th=self.th[0],
+                              lb_sub_th=self.th[1])
 
 
 class AttentionControl(abc.ABC):
@@ -326,11 +335,15 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
 
     def lb_buffer(self, frames: int, device) -> torch.Tensor:
         st = self.attention_store
+        sets = self.local_blend.sets
+        shape = (self.batch_size, frames, LB_HW[0] * LB_HW[1])
+        if sets > 1:
+            shape = (sets,) + shape
         if st.lb_acc is None:
-            st.lb_acc = torch.zeros(self.batch_size, frames, LB_HW[0] * LB_HW[1], device=device)
+            st.lb_acc = torch.zeros(shape, device=device)
             st.lb_layers_per_step = len(LB_SELECT["down"]) + len(LB_SELECT["up"])
-        elif st.lb_acc.shape[1] != frames:
-            raise ValueError(f"LocalBlend sum holds {st.lb_acc.shape[1]} frames, call has {frames}")
+        elif tuple(st.lb_acc.shape) != shape:
+            raise ValueError(f"LocalBlend sum is {tuple(st.lb_acc.shape)}, this call needs {shape}")
         return st.lb_acc
 
     def blend_plan(self) -> Optional[torch.Tensor]:
@@ -412,11 +425,13 @@ def get_equalizer(text: str, word_select, values, tokenizer) -> torch.Tensor:
 
 def make_controller(prompts: List[str], is_replace_controller: bool, cross_replace_steps: Dict[str, float],
                     self_replace_steps: float, blend_words=None, equilizer_params=None, mask_th=(.3, .3),
-                    tokenizer=None, num_steps: int = NUM_DDIM_STEPS, store_maps: bool = False) -> AttentionControlEdit:
+                    tokenizer=None, num_steps: int = NUM_DDIM_STEPS, store_maps: bool = False,
+                    substruct_words=None) -> AttentionControlEdit:
     """run_videop2p.py:397-410 (the reference reads ``blend_words`` from main's ``blend_word``
-    closure; here it is the argument)."""
-    lb = None if blend_words is None else LocalBlend(prompts, blend_words, tokenizer, th=mask_th,
-                                                       num_steps=num_steps)
+    closure; here it is the argument).  ``substruct_words`` is passed to LocalBlend
+    (run_videop2p.py:157, 166-174; the reference's factory never sets it)."""
+    lb = None if blend_words is None else LocalBlend(prompts, blend_words, tokenizer, substruct_words=substruct_words,
+                                                       th=mask_th, num_steps=num_steps)
     cls = AttentionReplace if is_replace_controller else AttentionRefine
     controller = cls(prompts, num_steps, cross_replace_steps=cross_replace_steps,
                      self_replace_steps=self_replace_steps, local_blend=lb, tokenizer=tokenizer,

@@ -170,8 +170,13 @@ class CrossEditPlan:
                 prompts - 1, tokens_kv).contiguous().to(dev)
         self.equalizer = (None if equalizer is None else
                           torch.as_tensor(equalizer, dtype=torch.float32).reshape(-1)[:tokens_kv].contiguous().to(dev))
+        # (sets, prompts, 77): set 0 = LocalBlend's blend words, set 1 = its substruct_words (optional)
         self.lb_word_alpha = (None if lb_word_alpha is None else
-                              torch.as_tensor(lb_word_alpha, dtype=torch.float32).reshape(prompts, tokens_kv).contiguous().to(dev))
+                              torch.as_tensor(lb_word_alpha, dtype=torch.float32).reshape(-1, prompts, tokens_kv)
+                              .contiguous().to(dev))
+        self.lb_sets = 0 if self.lb_word_alpha is None else self.lb_word_alpha.shape[0]
+        if self.lb_sets > 2:
+            raise ValueError("LocalBlend word weights: at most 2 sets (blend words, substruct words)")
 
     def alpha_ptr(self, step: int):
         return ctypes.c_void_p(self.alpha_steps[step].data_ptr())
@@ -210,6 +215,12 @@ def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frame
     q_sb, q_sf, q_sn = _bf_strides(q, frames)
     o_sb, o_sf, o_sn = _bf_strides(out, frames)
     P = plan.prompts if plan is not None else prompts
+    sets = 1
+    if lb_acc is not None:      # (P, f, N), or (sets, P, f, N) with the substruct_words set
+        sets = plan.lb_sets if plan is not None else 0
+        shape = (P, frames, N) if sets == 1 else (sets, P, frames, N)
+        if sets < 1 or tuple(lb_acc.shape) != shape or not lb_acc.is_contiguous() or lb_acc.dtype != torch.float32:
+            raise ValueError(f"lb_acc must be a contiguous fp32 {shape} tensor")
     mode = plan.edit_mode if (plan is not None and edit) else _lib.EDIT_NONE
     rew = int(plan.reweight) if (plan is not None and edit) else 0
     a = _lib.CrossAttnArgs(_ptr(q), _ptr(ws), _ptr(out), q_sb, q_sf, q_sn, o_sb, o_sf, o_sn,
@@ -222,9 +233,11 @@ def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frame
                            _ptr(plan.refine_alpha) if plan is not None else None,
                            _ptr(plan.equalizer) if plan is not None else None,
                            _ptr(lb_acc), _ptr(plan.lb_word_alpha) if (plan is not None and lb_acc is not None) else None,
-                           _ptr(probs_out),
-                           _ptr(torch.empty(P * heads * frames * N, device=q.device, dtype=torch.float32))
-                           if lb_acc is not None else None)
+                           _ptr(probs_out), None, sets)
+    lb_ws = None
+    if lb_acc is not None:       # per-head partials, reduced in head order by the library's second pass
+        lb_ws = torch.empty(sets * P * heads * frames * N, device=q.device, dtype=torch.float32)
+        a.lb_ws = _ptr(lb_ws)
     check(_lib.load().vp2p_cross_attn_p2p_fwd(ctypes.byref(a), _stream()), "vp2p_cross_attn_p2p_fwd")
     return out
 
@@ -271,9 +284,12 @@ def temporal_attention_p2p_bd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
 # ----------------------------------------------------------------------------------------------
 def step_fused(noise: torch.Tensor, latents: torch.Tensor, consts, guidance: float = 7.5, cfg: bool = True,
                fast: bool = False, lb_acc: Optional[torch.Tensor] = None, lb_hw=(16, 16),
-               lb_count: float = 40.0, lb_th: float = 0.3, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+               lb_count: float = 40.0, lb_th: float = 0.3, out: Optional[torch.Tensor] = None,
+               lb_sub_th: float = 0.3) -> torch.Tensor:
     """CFG + DDIM update + LocalBlend in one launch.  noise: (2P or P, C, f, H, W) bf16/f32,
-    latents: (P, C, f, H, W) fp32, consts = (c1, c2, c3, c4) float32 scalars."""
+    latents: (P, C, f, H, W) fp32, consts = (c1, c2, c3, c4) float32 scalars.  ``lb_acc``: the
+    LocalBlend sums, (P, f, h*w) or (sets, P, f, h*w) with set 1 = the substruct_words sum
+    (thresholded at ``lb_sub_th`` without pooling, run_videop2p.py:149-151)."""
     if not (noise.is_cuda and latents.is_cuda):
         raise RuntimeError("step_fused runs on the GPU only")
     if latents.dtype != torch.float32 or not latents.is_contiguous() or not noise.is_contiguous():
@@ -284,9 +300,19 @@ def step_fused(noise: torch.Tensor, latents: torch.Tensor, consts, guidance: flo
     if out is None:
         out = torch.empty_like(latents)
     c1, c2, c3, c4 = (float(c) for c in consts)
+    lb_sub = None
+    if lb_acc is not None:
+        if lb_acc.dim() == 4:
+            if lb_acc.shape[0] == 2:
+                lb_sub = lb_acc[1]
+            lb_acc = lb_acc[0]
+        if tuple(lb_acc.shape) != (P, F, int(lb_hw[0]) * int(lb_hw[1])) or not lb_acc.is_contiguous():
+            raise ValueError(f"lb_acc: expected contiguous {(P, F, int(lb_hw[0]) * int(lb_hw[1]))}, "
+                             f"got {tuple(lb_acc.shape)}")
     a = _lib.StepArgs(_ptr(noise), _DT[noise.dtype], _ptr(latents), _ptr(out), P, C, F, H, W,
                       int(cfg), int(fast), float(guidance), c1, c2, c3, c4,
-                      _ptr(lb_acc), int(lb_hw[0]), int(lb_hw[1]), float(lb_count), float(lb_th))
+                      _ptr(lb_acc), int(lb_hw[0]), int(lb_hw[1]), float(lb_count), float(lb_th),
+                      _ptr(lb_sub), float(lb_sub_th))
     check(_lib.load().vp2p_step_fused(ctypes.byref(a), _stream()), "vp2p_step_fused")
     return out
 

@@ -56,7 +56,10 @@ class VideoP2PPipeline:
                  num_inference_steps: int = NUM_DDIM_STEPS, guidance_scale: float = GUIDANCE_SCALE,
                  latents: Optional[torch.Tensor] = None, uncond_embeddings_pre=None, controller=None,
                  fast: bool = False, eta: float = 0.0, text_embeddings: Optional[torch.Tensor] = None,
-                 generator=None, output_type: str = "latent", **kwargs):
+                 generator=None, output_type: str = "latent", callback=None, callback_steps: int = 1,
+                 **kwargs):
+        """``callback(i, t, latents)`` runs after every ``callback_steps``-th step's update (and
+        LocalBlend), as in pipeline_tuneavideo.py:427-430."""
         if eta != 0.0:
             raise NotImplementedError("eta > 0 is out of scope (deterministic DDIM only)")
         if output_type != "latent":
@@ -71,9 +74,9 @@ class VideoP2PPipeline:
             latents = torch.randn(shape, generator=generator, dtype=torch.float32).to(dev)
         lat = latents.to(dev, torch.float32).expand(shape).contiguous() * self.scheduler.init_noise_sigma
         fused = controller is not None and hasattr(controller, "blend_plan")
-        lb_th = 0.3
+        lb_th = (0.3, 0.3)
         if fused and controller.local_blend is not None:
-            lb_th = controller.local_blend.th[0]
+            lb_th = controller.local_blend.th
         for i, t in enumerate(self.scheduler.timesteps.tolist()):
             if uncond_embeddings_pre is not None:
                 emb[0] = uncond_embeddings_pre[i]
@@ -82,7 +85,7 @@ class VideoP2PPipeline:
             if fused or controller is None:
                 acc = controller.blend_plan() if fused else None
                 lat = ops.step_fused(noise, lat, self.scheduler.step_constants(t), guidance_scale, cfg=True,
-                                     fast=fast, lb_acc=acc, lb_count=40.0, lb_th=lb_th)
+                                     fast=fast, lb_acc=acc, lb_count=40.0, lb_th=lb_th[0], lb_sub_th=lb_th[1])
             else:  # foreign controller: reference order, step_callback on the new latents
                 u, c = noise.float().chunk(2)
                 e = u + guidance_scale * (c - u)
@@ -90,6 +93,8 @@ class VideoP2PPipeline:
                     e[0] = c[0]
                 lat = self.scheduler.step(e.contiguous(), t, lat).prev_sample
                 lat = controller.step_callback(lat).to(dev, torch.float32)
+            if callback is not None and i % callback_steps == 0:
+                callback(i, t, lat)
         return lat
 
 
