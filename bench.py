@@ -6,31 +6,40 @@ One "step" = one complete edit of one clip: 50 denoising steps of the UNet3D at 
 configs/rabbit-jump-p2p.yaml), fast mode, DDIM eta = 0 -- configs[1] of BASELINE.json
 ("rabbit-jump-p2p 8f 512^2 on 1xMI355X bf16").  Synthetic data: random-init SD-1.5-geometry
 UNet3D (seed 0, N(0, 0.02), attn_temp.to_out non-zero), random text embeddings standing in for
-CLIP (seed 1; CLIP and VAE are excluded from the metric), x_T ~ N(0, 1) (seed 2 + rank).
+CLIP (seed 1; CLIP and VAE are excluded from the metric), x_T ~ N(0, 1) (seed 2).
 
-Multi-GPU (torchrun): every rank edits its own clip, no data-path collective (scaling "weak");
-value = clips * frames / max-over-ranks wall time.
+Multi-GPU: ``python bench.py --gpus N`` starts N rank processes itself (a torchrun child, launched
+before this process touches the GPU); under an external torchrun it reads RANK / WORLD_SIZE.  The
+default ``--shard frames`` runs ONE clip over all ranks (strong scaling, frame_parallel.EditLayout):
+the CFG halves on two rank groups, the frames sharded inside each half, RCCL carrying the frame-0
+hidden-state broadcast, the 5-D GroupNorm statistics and the attn_temp all-to-all.  value = frames
+/ max-over-ranks wall time.  ``--shard clips``: every rank edits its own clip (weak scaling); it is
+also reported as the secondary ``clip_parallel`` field of a frame-sharded run.
 
-The JSON line also carries the live roofline of K1 (frame attention, the dominant, MFMA-bound
-kernel: its res-64 launch timed with HIP events on the launch stream during the timed region) and
-a CPU baseline (rank 0, N = 1): the oracle's fp32 CPU path on a bounded per-block sample,
-extrapolated to the same edit.
+The JSON line carries, measured live with HIP events on the launch stream inside the timed region:
+``roofline`` for K1 (frame attention, the dominant MFMA-bound kernel: its res-64 launches),
+``attention`` (K2 / K3 HBM rates and the aggregate attention MFMA utilisation over every K1/K2/K3
+launch), plus -- at N = 1 -- the 50-step DDIM inversion rate, a reference-precision fp32 edit and
+the CPU baseline (the oracle's fp32 UNet on the host cores, bounded sample, extrapolated).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "video-p2p_amd"))
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
-PEAK_F32_TFLOPS = 157.3
+PEAK_F32_TFLOPS = 157.3        # dense fp32 MFMA
+PEAK_HBM_GBS = 8000.0
 RABBIT = (["a rabbit is jumping on the grass", "a origami rabbit is jumping on the grass"],
           False, (("rabbit",), ("rabbit",)), {"words": ["origami"], "values": [2]}, 0.2, 0.5)
 # The other reference edits (configs/*-p2p.yaml; cross 0.2 / self 0.5 are run_videop2p.py's defaults).
@@ -57,12 +66,16 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--ddim-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-k1-events", action="store_true")
-    ap.add_argument("--mode", default="edit", choices=["edit", "nulltext", "k1long"],
+    ap.add_argument("--no-events", "--no-k1-events", dest="no_events", action="store_true",
+                    help="do not bracket the attention launches with HIP events")
+    ap.add_argument("--extras", default="auto", choices=["auto", "none", "all"],
+                    help="secondary lines: inversion + fp32 edit (N = 1), clip-parallel (N > 1); auto = those")
+    ap.add_argument("--mode", default="edit", choices=["edit", "nulltext", "k1long", "selftest"],
                     help="edit: the P2P edit (BASELINE metric, configs[1]); nulltext: official-mode inversion "
                          "(DDIM inversion + null-text optimisation, configs[3]), one step = one inversion; "
                          "k1long: configs[4], the FrameAttention of one UNet forward over a --long-frames clip "
-                         "at 768^2, frames sharded over the ranks with the RCCL frame-0 K/V broadcast")
+                         "at 768^2, frames sharded over the ranks; selftest: the launcher and the rank "
+                         "layout's collectives on the CPU (gloo), no GPU")
     ap.add_argument("--long-frames", type=int, default=128, help="k1long: frames of the clip")
     ap.add_argument("--conv-find", type=int, default=0,
                     help="1: run MIOpen's solver search per new conv shape (torch.backends.cudnn.benchmark; slow "
@@ -71,113 +84,168 @@ def parse():
     ap.add_argument("--tuned", type=int, default=1,
                     help="1 (default): in-tree tuned MIOpen database (vp2p.tuning); 0: library heuristics")
     ap.add_argument("--inner-steps", type=int, default=10, help="null-text Adam iterations per DDIM step")
-    ap.add_argument("--shard", default="clips", choices=["clips", "frames"],
-                    help="clips: every rank edits its own clip (weak scaling, no collective); "
-                         "frames: one clip's frames split over the ranks (strong scaling, RCCL)")
+    ap.add_argument("--shard", default="frames", choices=["frames", "clips"],
+                    help="frames (default): one clip over all ranks (CFG split x frame sharding, strong "
+                         "scaling); clips: every rank edits its own clip (weak scaling, no collective)")
     return ap.parse_args()
 
 
-class K1Timer:
-    """Brackets every res-64 FrameAttention launch with HIP events on the launch stream."""
+# -- launcher -------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    def __init__(self, ops, tokens=4096):
-        self.ops, self.tokens, self.orig = ops, tokens, ops.frame_attention
-        self.events, self.active = [], False
+
+def launch_ranks(n: int, argv) -> int:
+    """Start ``n`` rank processes of this script under torchrun (a CHILD process: this one has not
+    touched the GPU and never execs) and return the launcher's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# -- live kernel timing -----------------------------------------------------------------------------------
+class AttnTimer:
+    """Brackets every attention launch (K1 frame, K2 cross + P2P, K3 temporal) with HIP events on
+    the launch stream while ``active``; ``summary`` turns them into algorithmic rates."""
+
+    NAMES = ("frame_attention", "cross_attention_p2p", "temporal_attention_p2p")
+
+    def __init__(self, ops, enabled=True):
+        self.ops, self.enabled = ops, enabled
+        self.orig = {n: getattr(ops, n) for n in self.NAMES}
+        self.events = {n: [] for n in self.NAMES}
+        self.active = False
 
     def __enter__(self):
-        orig = self.orig
+        for name in self.NAMES:
+            orig = self.orig[name]
 
-        def wrapped(q, *a, **k):
-            if not self.active or q.shape[1] != self.tokens:
-                return orig(q, *a, **k)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            out = orig(q, *a, **k)
-            e.record()
-            self.events.append((s, e, tuple(q.shape)))
-            return out
-
-        self.ops.frame_attention = wrapped
-        import vp2p.attention as att
-        att.ops.frame_attention = wrapped
+            def wrapped(q, k, v, frames, heads, *a, _orig=orig, _name=name, **kw):
+                if not (self.active and self.enabled):
+                    return _orig(q, k, v, frames, heads, *a, **kw)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                out = _orig(q, k, v, frames, heads, *a, **kw)
+                e.record()
+                self.events[_name].append((s, e, tuple(q.shape), tuple(k.shape), frames, q.element_size()))
+                return out
+            setattr(self.ops, name, wrapped)
         return self
 
     def __exit__(self, *exc):
-        self.ops.frame_attention = self.orig
+        for name, fn in self.orig.items():
+            setattr(self.ops, name, fn)
 
-    def summary(self, frames, peak):
-        if not self.events:
-            return None
-        ms = [s.elapsed_time(e) for s, e, _ in self.events]
-        Bf, N, C = self.events[0][2]
-        flops = 4.0 * Bf * N * N * C           # QK^T + PV, frame-0 K/V: 4 * B*f * HW^2 * C
-        avg_s = sum(ms) / len(ms) / 1e3
-        achieved = flops / avg_s / 1e12
-        esz = 2 if peak == PEAK_BF16_TFLOPS else 4
-        alg_bytes = esz * (2 * Bf * N * C + 2 * (Bf // frames) * N * C)   # Q in + O out + frame-0 K, V
-        traffic, src = _pmc_traffic()
-        return {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": src, "algorithmic_bytes": alg_bytes,
-                "kernel": "vp2p::frame_attn_kernel_x2f<40,256> (res-64 FrameAttention, bf16)",
-                "launches": len(ms), "avg_ms": round(sum(ms) / len(ms), 4),
-                "flops_per_launch": flops}
+    @staticmethod
+    def _work(name, qs, ks, frames, esz):
+        """(algorithmic FLOP, algorithmic HBM bytes) of one launch."""
+        Bf, N, C = qs
+        B = Bf // frames
+        if name == "frame_attention":       # QK^T + PV against frame-0 K/V; Q, O + frame-0 K, V once
+            Nk = ks[1]
+            return 4.0 * Bf * N * Nk * C, esz * (2 * Bf * N * C + 2 * B * Nk * C)
+        if name == "cross_attention_p2p":   # 77 keys; Q in, O out, K/V once per batch row
+            Nk = ks[1]
+            return 4.0 * Bf * N * Nk * C, esz * (2 * Bf * N * C + 2 * B * Nk * C)
+        # temporal: f x f per token; Q, K, V in, O out
+        return 4.0 * Bf * N * frames * C, esz * 4 * Bf * N * C
+
+    def summary(self, peak):
+        if not any(self.events.values()):
+            return None, None
+        stats = {}
+        tot_flop = tot_ms = 0.0
+        for name, evs in self.events.items():
+            if not evs:
+                continue
+            ms = [s.elapsed_time(e) for s, e, *_ in evs]
+            flop = sum(self._work(name, qs, ks, f, esz)[0] for _, _, qs, ks, f, esz in evs)
+            tot_flop += flop
+            tot_ms += sum(ms)
+            # the largest-token launches (res-64 at 512^2) are the headline shape of each kernel
+            top = max(qs[1] for _, _, qs, *_ in evs)
+            sel = [(m, ev) for m, ev in zip(ms, evs) if ev[2][1] == top]
+            avg_ms = sum(m for m, _ in sel) / len(sel)
+            f1, b1 = self._work(name, sel[0][1][2], sel[0][1][3], sel[0][1][4], sel[0][1][5])
+            stats[name] = {"launches": len(evs), "time_ms": round(sum(ms), 2), "tokens": top,
+                           "avg_ms": round(avg_ms, 4), "flop_per_launch": f1, "bytes_per_launch": b1,
+                           "tflops": round(f1 / avg_ms / 1e9, 1), "gbs": round(b1 / avg_ms / 1e6, 1),
+                           "shape": list(sel[0][1][2])}
+        k1 = stats.get("frame_attention")
+        roof = None
+        if k1:
+            traffic, src = _pmc_traffic(k1["shape"])
+            roof = {"bound": "mfma", "achieved": k1["tflops"], "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(k1["tflops"] / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                    "traffic_source": src, "algorithmic_bytes": k1["bytes_per_launch"],
+                    "kernel": "vp2p::frame_attn_kernel_x2f<40,256> (res-64 FrameAttention)",
+                    "launches": sum(1 for ev in self.events["frame_attention"] if ev[2][1] == k1["tokens"]),
+                    "avg_ms": k1["avg_ms"], "flops_per_launch": k1["flop_per_launch"], "shape": k1["shape"]}
+        attn = {"mfma_util": round(tot_flop / (tot_ms / 1e3) / 1e12 / peak, 4),
+                "flop_per_edit_step_total": tot_flop, "kernel_ms_total": round(tot_ms, 2)}
+        for key, name in (("k2_cross", "cross_attention_p2p"), ("k3_temporal", "temporal_attention_p2p")):
+            if name in stats:
+                st = stats[name]
+                attn[key] = {"bound": "hbm", "achieved_gbs": st["gbs"], "peak_gbs": PEAK_HBM_GBS,
+                             "frac": round(st["gbs"] / PEAK_HBM_GBS, 4), "avg_ms": st["avg_ms"],
+                             "bytes_per_launch": st["bytes_per_launch"], "shape": st["shape"],
+                             "launches": st["launches"]}
+        if k1:
+            attn["k1_frame"] = {"tflops": k1["tflops"], "frac": round(k1["tflops"] / peak, 4)}
+        return roof, attn
 
 
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "k1_pmc_traffic.json")
 
 
-def _pmc_traffic():
-    """HBM bytes per K1 launch from the committed rocprofv3 --pmc passes (FETCH_SIZE x2 per the gfx950
-    correction, + WRITE_SIZE; tools/pmc_traffic.py) on the same kernel and shape, or None."""
+def _pmc_traffic(shape):
+    """HBM bytes per K1 launch from committed rocprofv3 --pmc passes (FETCH_SIZE x2 per the gfx950
+    correction, + WRITE_SIZE; tools/pmc_traffic.py) -- only when they were taken on this exact
+    launch shape; otherwise None (the counters are not readable from inside the process)."""
     try:
         with open(TRAFFIC_FILE) as fh:
             d = json.load(fh)
+        if list(d.get("shape", [])) != list(shape):
+            return None, f"no PMC pass for shape {list(shape)} (profiles/k1_pmc_traffic.json is {d.get('shape')})"
         return d["bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT) + " (" + d["how"] + ")"
     except (OSError, KeyError, ValueError):
         return None, None
 
 
-def cpu_baseline(frames, ddim_steps, threads):
-    """Oracle fp32 CPU path on a bounded sample: one transformer block and one resnet block per
-    resolution level of the B=4 edit UNet, extrapolated by the block counts of one forward and x50."""
-    import numpy as np
+# -- CPU baseline -----------------------------------------------------------------------------------------
+def cpu_baseline(frames, ddim_steps, sample_frames=2):
+    """The oracle's fp32 CPU UNet (oracle/unet_ref.py: the reference math, pinned to the reference's
+    own model files) for ONE complete UNet forward of the edit (B = 4, every layer: 16 transformer
+    blocks with the controller, 22 resnets, the up/down-sample convs) on ``sample_frames`` frames,
+    timed once on this host's CPU share and extrapolated to ``frames`` x ``ddim_steps``.  Every
+    per-frame cost is linear in the frame count (frame attention reads frame 0's K/V; the temporal
+    f x f attention is < 0.1% of the FLOPs)."""
     from oracle import p2p_oracle as O
     from oracle import unet_ref
     from vp2p.tokenizer import SyntheticCLIPTokenizer
     from vp2p.unet3d import UNet3DConditionModel, init_random_
-    torch.set_num_threads(threads)
+    threads = torch.get_num_threads()
     prompts, swap, blend, eq, cross, self_ = RABBIT
-    tok = SyntheticCLIPTokenizer()
-    ctrl = O.EditController(prompts, swap, {"default_": cross}, self_, tok, blend_words=blend, eq_params=eq)
-    sd = {k: v for k, v in init_random_(UNet3DConditionModel(), seed=0).state_dict().items()}
+    ctrl = O.EditController(prompts, swap, {"default_": cross}, self_, SyntheticCLIPTokenizer(),
+                            blend_words=blend, eq_params=eq)
+    sd = init_random_(UNet3DConditionModel(), seed=0).state_dict()
     g = torch.Generator().manual_seed(3)
-    B = 4
-    ctx = torch.randn(B, 77, 768, generator=g)
-    emb = torch.randn(B, 1280, generator=g)
-    # (prefix of a transformer, prefix of a resnet, channels, latent size, transformers, resnets per forward)
-    levels = [("down_blocks.0.attentions.0.", "down_blocks.0.resnets.1.", 320, 64, 5, 5),
-              ("down_blocks.1.attentions.0.", "down_blocks.1.resnets.1.", 640, 32, 5, 5),
-              ("down_blocks.2.attentions.0.", "down_blocks.2.resnets.1.", 1280, 16, 5, 5),
-              ("mid_block.attentions.0.", "mid_block.resnets.0.", 1280, 8, 1, 7)]
-    t_fwd, t_sample = 0.0, 0.0
-    for tp, rp, C, hw, n_t, n_r in levels:
-        x = torch.randn(B, C, frames, hw, hw, generator=g) * 0.5
+    x = torch.randn(4, 4, sample_frames, 64, 64, generator=g)
+    ctx = torch.randn(4, 77, 768, generator=g)
+    with torch.no_grad():
         t0 = time.perf_counter()
-        with torch.no_grad():
-            unet_ref.transformer(sd, tp, x, ctx, ctrl, "down")
-        t1 = time.perf_counter()
-        with torch.no_grad():
-            unet_ref.resnet(sd, rp, x, emb)
-        t2 = time.perf_counter()
-        t_fwd += n_t * (t1 - t0) + n_r * (t2 - t1)
-        t_sample += t2 - t0
-    t_edit = t_fwd * ddim_steps
+        unet_ref.unet_forward(sd, x, 981, ctx, ctrl)
+        t_fwd = time.perf_counter() - t0
+    t_edit = t_fwd * (frames / sample_frames) * ddim_steps
     return {"value": round(frames / t_edit, 6), "unit": "edited frames/s", "cores": threads, "kind": "port",
-            "sample": (f"oracle/unet_ref.py fp32 on host CPU: 1 transformer block + 1 resnet block per level "
-                       f"(B=4, f={frames}, 512^2) timed once ({t_sample:.1f} s), extrapolated by block counts to "
-                       f"one UNet forward ({t_fwd:.1f} s) x {ddim_steps} steps; excludes up/downsample convs"),
-            "cpu_model": _cpu_model()}
+            "sample": (f"oracle/unet_ref.py fp32 (pinned to tuneavideo's model files): one full UNet3D forward of the "
+                       f"edit (B=4, {sample_frames} frames, 512^2, rabbit controller) timed once ({t_fwd:.1f} s), "
+                       f"x{frames / sample_frames:g} frames x {ddim_steps} steps (extrapolated)"),
+            "torch_threads": threads, "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
 
 
 def _cpu_model():
@@ -190,13 +258,15 @@ def _cpu_model():
     return "unknown"
 
 
+# -- other modes ----------------------------------------------------------------------------------------
 def k1long_main(args, world, rank, dev):
     """configs[4] of BASELINE.json: sparse-causal (first-frame K/V) attention of a 128-frame 768^2
     clip, sharded by frames over the ranks.  One step = every attn1 call of one UNet forward at
     UNet batch 4 (5 blocks at 96^2 tokens / C 320, 5 at 48^2 / 640, 5 at 24^2 / 1280, 1 at 12^2 / 1280):
-    per call rank 0 (owner of frame 0) broadcasts the frame-0 K/V (B, HW, 2C) over RCCL, then every
-    rank runs K1 on its f/G frames.  Synthetic bf16 activations; the projections are not timed."""
+    per call rank 0 (owner of frame 0) broadcasts the frame-0 normed hidden state (B, HW, C) over
+    RCCL, every rank projects frame 0's K|V and runs K1 on its f/G frames.  Synthetic bf16."""
     import torch.distributed as dist
+    import torch.nn.functional as F
     from vp2p import ops
     B, heads, f = 4, 8, args.long_frames
     if f % world:
@@ -207,14 +277,16 @@ def k1long_main(args, world, rank, dev):
     bufs = []
     for hw, C, n in levels:
         q = torch.randn(B * fl, hw, C, device=dev, dtype=torch.bfloat16, generator=g)
-        kv = torch.randn(B, hw, 2 * C, device=dev, dtype=torch.bfloat16, generator=g)
-        bufs.append((q, kv, torch.empty_like(q), C, n))
+        x0 = torch.randn(B, hw, C, device=dev, dtype=torch.bfloat16, generator=g)
+        wkv = torch.randn(2 * C, C, device=dev, dtype=torch.bfloat16, generator=g) * C ** -0.5
+        bufs.append((q, x0, wkv, torch.empty_like(q), C, n))
 
     def step():
-        for q, kv, out, C, n in bufs:
+        for q, x0, wkv, out, C, n in bufs:
             for _ in range(n):
                 if world > 1:
-                    dist.broadcast(kv, src=0)
+                    dist.broadcast(x0, src=0)
+                kv = F.linear(x0, wkv)
                 ops.frame_attention(q, kv[..., :C], kv[..., C:], fl, heads, out=out)
 
     for _ in range(args.warmup):
@@ -228,25 +300,21 @@ def k1long_main(args, world, rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = _max_over_ranks(time.perf_counter() - t0, world, dev)
     flops = sum(4.0 * B * f * hw * hw * C * n for hw, C, n in levels)
     result = {
-        "metric": "sparse-causal attention TFLOP/s, 768^2 x 128-frame clip (K1 + RCCL frame-0 K/V broadcast)",
+        "metric": "sparse-causal attention TFLOP/s, 768^2 x 128-frame clip (K1 + RCCL frame-0 hidden broadcast)",
         "value": round(flops * args.steps / elapsed / 1e12, 1), "unit": "TFLOP/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random bf16 q / frame-0 k,v)",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random bf16 q / frame-0 hidden / K|V weights)",
         "config": {"workload": f"attn1 of one UNet forward, {f} frames 768^2, UNet batch {B}, frame-sharded x{world}",
                    "frames": f, "resolution": 768, "unet_batch": B, "parallelism": f"frame-sharded x{world} (RCCL)"},
         "frames_per_s": round(f * args.steps / elapsed, 2),
         "roofline": {"bound": "mfma", "achieved": round(flops / world * args.steps / elapsed / 1e12, 1),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(flops / world * args.steps / elapsed / 1e12 / PEAK_BF16_TFLOPS, 4),
-                     "note": "per-GPU K1 algorithmic FLOP rate including the broadcast time"},
+                     "note": "per-GPU K1 algorithmic FLOP rate including the broadcast and K|V projection time"},
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -273,19 +341,13 @@ def nulltext_main(args, world, rank, dev):
     for _ in range(args.warmup):
         run(2)
     torch.cuda.synchronize()
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
+    _barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         _, x_t, unc = run(args.ddim_steps)
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    _barrier(world)
+    elapsed = _max_over_ranks(time.perf_counter() - t0, world, dev)
     result = {
         "metric": "null-text inverted frames/sec (DDIM inversion + null-text optimisation, 512^2)",
         "value": round(args.frames * args.steps * world / elapsed, 5), "unit": "inverted frames/s",
@@ -303,6 +365,53 @@ def nulltext_main(args, world, rank, dev):
         print(json.dumps(result), flush=True)
 
 
+def selftest_main(args, world, rank):
+    """CPU (gloo) rehearsal of the multi-rank path: the launcher brought up ``world`` ranks; build the
+    EditLayout and run each of its exchanges on CPU tensors against the single-rank answer."""
+    import torch.distributed as dist
+    from vp2p.frame_parallel import EditLayout
+    lay = EditLayout()
+    P, f, N, C = 2, 8, 16, 6
+    g = torch.Generator().manual_seed(7)
+    full = torch.randn(2 * P, 4, f, 8, 8, generator=g)              # [uncond x P, cond x P] noise
+    fl = lay.frames_local(f)
+    half = lay.half if lay.cfg_split else None
+    rows = full if half is None else full[half * P:(half + 1) * P]
+    mine = lay.local(rows, 2)
+    got = lay.gather_cfg(mine)
+    want = lay.local(full, 2) if half is not None else mine
+    ok = torch.equal(got, want)
+    if lay.frames is not None:                                          # frame-0 hidden broadcast
+        x0 = torch.full((2, N, C), float(lay.rank)) if lay.frames.rank else torch.full((2, N, C), -1.0)
+        lay.frames.broadcast_(x0)
+        ok &= bool((x0 == -1.0).all())
+        x = torch.randn(2 * fl, N, C, generator=torch.Generator().manual_seed(11 + lay.frame_rank))
+        ok &= torch.equal(lay.frames.to_frames(lay.frames.to_tokens(x, 2), 2), x)
+    t = torch.tensor([float(ok)])
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print(json.dumps({"selftest": "ok" if t.item() == 1.0 else "FAILED", "world": world,
+                          "layout": lay.describe(), "frames_local": fl}), flush=True)
+    if t.item() != 1.0:
+        raise SystemExit(1)
+
+
+# -- helpers ----------------------------------------------------------------------------------------------
+def _barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def _max_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def _heartbeat(period=30.0):
     """A line on stderr every `period` s, so a long run (first use of new conv shapes, 24 frames) is
     never mistaken for a hung one."""
@@ -316,16 +425,104 @@ def _heartbeat(period=30.0):
     threading.Thread(target=beat, daemon=True).start()
 
 
+class Edit:
+    """One edit configuration (model, controller, inputs) ready to run under a layout."""
+
+    def __init__(self, args, dev, dtype, layout=None, seed_offset=0):
+        import vp2p
+        from vp2p.pipeline import VideoP2PPipeline
+        from vp2p.tokenizer import SyntheticCLIPTokenizer
+        from vp2p.unet3d import UNet3DConditionModel, init_random_
+        self.f = args.frames
+        self.steps = args.ddim_steps
+        name, kind, (prompts, swap, blend, eq, cross, self_) = EDITS[args.edit]
+        self.name, self.kind, self.prompts = name, kind, prompts
+        self.unet = init_random_(UNet3DConditionModel(), seed=0).to(dev, dtype).to(memory_format=torch.channels_last)
+        self.unet.eval()
+        self.ctrl = vp2p.make_controller(prompts, swap, {"default_": cross}, self_, blend, eq,
+                                         tokenizer=SyntheticCLIPTokenizer(), num_steps=args.ddim_steps)
+        vp2p.register_attention_control(type("Pipe", (), {"unet": self.unet})(), self.ctrl)
+        g = torch.Generator().manual_seed(1)
+        unc = torch.randn(1, 77, 768, generator=g)
+        self.emb = torch.cat([unc, unc, torch.randn(2, 77, 768, generator=g)]).to(dev)
+        x_T = torch.randn(1, 4, self.f, 64, 64, generator=torch.Generator().manual_seed(2 + seed_offset)).to(dev)
+        self.layout = layout
+        self.x_T = layout.local(x_T, 2) if layout is not None else x_T
+        self.pipe = VideoP2PPipeline(self.unet)
+
+    def __call__(self):
+        from vp2p.frame_parallel import frame_parallel
+        self.ctrl.reset()
+        with frame_parallel(self.layout):
+            return self.pipe(self.prompts, self.x_T.shape[2], latents=self.x_T, controller=self.ctrl, fast=True,
+                             text_embeddings=self.emb, num_inference_steps=self.steps)
+
+
+def _time_edits(edit, warmup, steps, world, dev, timer=None):
+    for _ in range(warmup):
+        out = edit()
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+    if timer is not None:
+        timer.active = True
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = edit()
+    torch.cuda.synchronize()
+    _barrier(world)
+    t1 = time.perf_counter()
+    if timer is not None:
+        timer.active = False
+    return _max_over_ranks(t1 - t0, world, dev), out
+
+
+def inversion_line(edit, dev, reps=2):
+    """Fast-mode DDIM inversion (NullInversion.invert_, run_videop2p.py:626-635 / ddim_loop :557-567):
+    50 UNet forwards at batch 1 (DummyController), reported separately."""
+    import vp2p
+    from vp2p.pipeline import NullInversion, VideoP2PPipeline
+    unet = edit.unet
+    x0 = torch.randn(1, 4, edit.f, 64, 64, generator=torch.Generator().manual_seed(4)).to(dev)
+    ctx = edit.emb[[0, 2]].contiguous()                   # [uncond, cond of the source prompt]
+    inv = NullInversion(VideoP2PPipeline(unet), num_ddim_steps=edit.steps)
+    inv.invert_(x0, "", text_embeddings=ctx)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, x_t, _ = inv.invert_(x0, "", text_embeddings=ctx)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    vp2p.register_attention_control(type("Pipe", (), {"unet": unet})(), edit.ctrl)   # back to the edit
+    return {"metric": f"inverted frames/sec ({edit.steps}-step DDIM inversion, batch 1, 512^2)",
+            "value": round(edit.f / dt, 4), "unit": "inverted frames/s", "ms_per_inversion": round(dt * 1e3, 1),
+            "output_finite": bool(torch.isfinite(x_t).all().item())}
+
+
 def main():
     args = parse()
-    _heartbeat()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with matching counts")
+    if args.mode == "selftest":
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo")
+        try:
+            selftest_main(args, world, rank)
+        finally:
+            if world > 1:
+                dist.destroy_process_group()
+        return
+    _heartbeat()
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     torch.backends.cudnn.benchmark = bool(args.conv_find)
@@ -339,72 +536,21 @@ def main():
             dist.destroy_process_group()
         return
 
-    import vp2p
     from vp2p import ops
-    from vp2p.pipeline import VideoP2PPipeline
-    from vp2p.tokenizer import SyntheticCLIPTokenizer
-    from vp2p.unet3d import UNet3DConditionModel, init_random_
-
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    f = args.frames
-    edit_name, edit_kind, (prompts, swap, blend, eq, cross, self_) = EDITS[args.edit]
-    tok = SyntheticCLIPTokenizer()
-    unet = init_random_(UNet3DConditionModel(), seed=0).to(dev, dtype).to(memory_format=torch.channels_last)
-    unet.eval()
-    ctrl = vp2p.make_controller(prompts, swap, {"default_": cross}, self_, blend, eq, tokenizer=tok,
-                                num_steps=args.ddim_steps)
-    vp2p.register_attention_control(type("Pipe", (), {"unet": unet})(), ctrl)
-    g = torch.Generator().manual_seed(1)
-    unc = torch.randn(1, 77, 768, generator=g)
-    emb = torch.cat([unc, unc, torch.randn(2, 77, 768, generator=g)]).to(dev)
-    frames_mode = args.shard == "frames" and world > 1
-    x_T = torch.randn(1, 4, f, 64, 64,
-                      generator=torch.Generator().manual_seed(2 if frames_mode else 2 + rank)).to(dev)
-    pipe = VideoP2PPipeline(unet)
-    shard = None
-    if frames_mode:
-        from vp2p.frame_parallel import FrameShard
-        shard = FrameShard()
-        x_T = shard.local(x_T, 2)
-    f_run = x_T.shape[2]
-
-    def edit():
-        from vp2p.frame_parallel import frame_parallel
-        ctrl.reset()
-        with frame_parallel(shard):
-            return pipe(prompts, f_run, latents=x_T, controller=ctrl, fast=True, text_embeddings=emb,
-                        num_inference_steps=args.ddim_steps)
-
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            out = edit()
-        torch.cuda.synchronize()
-        timer = K1Timer(ops)
-        with timer:
-            timer.active = not args.no_k1_events
-            barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                out = edit()
-            torch.cuda.synchronize()
-            barrier()
-            t1 = time.perf_counter()
-            timer.active = False
-    elapsed = t1 - t0
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    finite = bool(torch.isfinite(out).all().item())
     peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
-    roof = timer.summary(f, peak)
+    frames_mode = args.shard == "frames" and world > 1
+    layout = None
+    if frames_mode:
+        from vp2p.frame_parallel import EditLayout
+        layout = EditLayout()
+    edit = Edit(args, dev, dtype, layout, seed_offset=0 if frames_mode else rank)
+    with torch.no_grad():
+        with AttnTimer(ops, enabled=not args.no_events) as timer:
+            elapsed, out = _time_edits(edit, args.warmup, args.steps, world, dev, timer)
+    finite = bool(torch.isfinite(out).all().item())
+    roof, attn = timer.summary(peak)
+    f = args.frames
     result = {
         "metric": "edited frames/sec, 50-step DDIM P2P 512^2; attn MFMA util % of gfx950 peak",
         "value": round(f * args.steps * (1 if frames_mode else world) / elapsed, 4),
@@ -413,16 +559,43 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "strong" if frames_mode else "weak", "vs_baseline": None,
         "dtype": args.dtype, "data": "synthetic (random-init SD-1.5-geometry UNet3D, random text embeddings, x_T~N(0,1))",
-        "config": {"workload": f"{edit_name} --fast: {edit_kind}, {f} frames 512^2, "
+        "config": {"workload": f"{edit.name} --fast: {edit.kind}, {f} frames 512^2, "
                                f"{args.ddim_steps}-step DDIM, UNet batch 4", "frames": f, "resolution": 512,
                    "ddim_steps": args.ddim_steps, "unet_batch": 4,
-                   "parallelism": f"frame-sharded x{world} (RCCL)" if frames_mode else f"clip-parallel x{world}"},
+                   "parallelism": (layout.describe() + " (RCCL)") if frames_mode else f"clip-parallel x{world}"},
         "roofline": roof,
+        "attention": attn,
         "output_finite": finite,
     }
+    extras = args.extras != "none"
+    with torch.no_grad():
+        if extras and world > 1 and frames_mode:
+            # secondary: every rank edits its own full clip (no collective), one timed edit
+            clip = Edit(args, dev, dtype, None, seed_offset=rank)
+            t_clip, _ = _time_edits(clip, 1, 1, world, dev)
+            result["clip_parallel"] = {"value": round(f * world / t_clip, 4), "ms_per_step": round(t_clip * 1e3, 2),
+                                       "scaling": "weak", "parallelism": f"clip-parallel x{world}"}
+            del clip
+        if extras and world == 1:
+            result["inversion"] = inversion_line(edit, dev)
+            if dtype == torch.bfloat16 and args.extras in ("auto", "all"):
+                del edit
+                torch.cuda.empty_cache()
+                ref_args = argparse.Namespace(**{**vars(args), "dtype": "fp32"})
+                e32 = Edit(ref_args, dev, torch.float32)
+                with AttnTimer(ops, enabled=not args.no_events) as t32:
+                    el32, out32 = _time_edits(e32, 1, 1, 1, dev, t32)
+                r32, a32 = t32.summary(PEAK_F32_TFLOPS)
+                result["fp32_edit"] = {"value": round(f / el32, 4), "unit": "edited frames/s",
+                                       "ms_per_step": round(el32 * 1e3, 1), "dtype": "fp32",
+                                       "note": "reference precision (run_videop2p.py:111-113 runs the UNet in fp32)",
+                                       "k1_frac_of_fp32_peak": None if r32 is None else r32["frac"],
+                                       "attn_mfma_util_fp32": None if a32 is None else a32["mfma_util"],
+                                       "output_finite": bool(torch.isfinite(out32).all().item())}
+                del e32
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(f, args.ddim_steps, min(16, os.cpu_count() or 1))
+            result["cpu_baseline"] = cpu_baseline(f, args.ddim_steps)
         except Exception as e:  # keep the GPU line even if the host leg fails
             result["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

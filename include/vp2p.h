@@ -126,6 +126,9 @@ typedef struct vp2p_cross_attn_args {
    * required when lb_acc is set (the head sum is finished in a fixed order by a second pass). */
   float* lb_ws;
   int32_t lb_sets;          /* word-weight sets accumulated: 1 (0 is read as 1) or 2 */
+  /* 1: the batch holds ONLY the conditional half (batch = prompts) -- a rank of a CFG-split edit
+   * (the unconditional rank runs with prompts = 0, i.e. plain attention); 0: batch = 2*prompts. */
+  int32_t cond_only;
 } vp2p_cross_attn_args;
 
 /* Bytes of the K/V workspace for one context of the given shape (<0: unsupported). */
@@ -153,6 +156,7 @@ typedef struct vp2p_temporal_attn_args {
   int32_t prompts;          /* batch = 2*prompts when self_replace is set */
   int32_t self_replace;     /* conditional rows of prompts 1.. use the source prompt's probs */
   float* probs_out;         /* ((batch*tokens*heads), frames, frames) fp32 in '(b d)' order, or NULL */
+  int32_t cond_only;        /* as vp2p_cross_attn_args.cond_only (batch = prompts, all conditional) */
 } vp2p_temporal_attn_args;
 
 int vp2p_temporal_attn_p2p_fwd(const vp2p_temporal_attn_args* args, void* stream);

@@ -122,3 +122,47 @@ def test_frame_sharded_unet_matches_single(tmp_path):
     assert err < 1e-4, float(err)
     lb_ref = ctrl.attention_store.lb_acc.cpu()
     assert ((got["lb"] - lb_ref).abs().max() / lb_ref.abs().max()) < 1e-4
+
+
+# ------------------------------------------------------------------------------------------------
+def _edit_worker(rank, world, port, out_path, frames, steps):
+    """A short fast-mode edit (LocalBlend on from the first step) under the bench's EditLayout:
+    world 2 = CFG split, world 4 = CFG split x 2 frame shards."""
+    dist = _init(rank, world, port)
+    from vp2p.frame_parallel import EditLayout, frame_parallel
+    from vp2p.pipeline import VideoP2PPipeline
+    import spec
+    unet, ctrl, x, ctx = _unet_case(frames)
+    ctrl.local_blend.start_blend = 0
+    lay = EditLayout()
+    with torch.no_grad(), frame_parallel(lay):
+        lat = VideoP2PPipeline(unet)(spec.CONFIGS["rabbit"][0], lay.frames_local(frames),
+                                     latents=lay.local(x[:1], 2), controller=ctrl, fast=True,
+                                     text_embeddings=ctx, num_inference_steps=steps)
+        if lay.frames is not None:
+            lat = lay.frames.gather(lat, 2)
+    torch.save(lat.cpu(), out_path + f".{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_cfg_split_edit_matches_single(tmp_path, world):
+    """The bench's multi-GPU decomposition (frame_parallel.EditLayout: CFG halves on two rank groups,
+    frames sharded inside each half; the per-step all-gather of the UNet outputs and the LocalBlend
+    broadcast) reproduces the single-rank edit.  All ranks share the one GPU (gloo, host staging)."""
+    frames, steps = 4, 3
+    out = str(tmp_path / "edit")
+    mp.spawn(_edit_worker, args=(world, _port(), out, frames, steps), nprocs=world, join=True)
+    sys.path.insert(0, os.path.join(ROOT, "video-p2p_amd"))
+    import spec
+    from vp2p.pipeline import VideoP2PPipeline
+    unet, ctrl, x, ctx = _unet_case(frames)
+    ctrl.local_blend.start_blend = 0
+    with torch.no_grad():
+        ref = VideoP2PPipeline(unet)(spec.CONFIGS["rabbit"][0], frames, latents=x[:1], controller=ctrl, fast=True,
+                                     text_embeddings=ctx, num_inference_steps=steps).cpu()
+    for r in range(world):
+        got = torch.load(out + f".{r}")
+        err = (got - ref).abs().max() / ref.abs().max()
+        assert err < 1e-4, (r, float(err))

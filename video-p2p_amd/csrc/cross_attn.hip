@@ -104,10 +104,10 @@ void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
   const int qblocks = (FQ + 31) >> 5;
   const int hgroups = (a.heads + 3) >> 2;
   const int items = qblocks * hgroups;
-  const bool p2p = a.prompts > 0 && a.batch == 2 * a.prompts;
+  const bool p2p = a.prompts > 0 && a.batch == (a.cond_only ? 1 : 2) * a.prompts;
   const int RP = p2p ? a.prompts : 1;          // rows per group
   const int g = blockIdx.y;                    // group: CFG half (p2p) or batch row
-  const bool cond = p2p && g == 1;
+  const bool cond = p2p && (a.cond_only || g == 1);   // cond_only: the one group is the conditional half
   const bool edit = cond && (a.edit_mode != VP2P_EDIT_NONE || a.reweight);
   const bool lb = cond && a.lb_acc != nullptr;
   const int NKV = a.tokens_kv;
@@ -359,8 +359,8 @@ static int cross_pad_dims(int head_dim, int dtype, int& dp, int& dv) {
 template <typename T, int D, int KB>
 static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
   const int FQ = a->frames * a->tokens_q;
-  const bool p2p = a->prompts > 0 && a->batch == 2 * a->prompts;
-  const int groups = p2p ? 2 : a->batch;
+  const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
+  const int groups = p2p ? (a->cond_only ? 1 : 2) : a->batch;
   const int64_t items = (int64_t)((FQ + 31) / 32) * ((a->heads + 3) / 4);
   if (items <= 0 || groups > 65535) return VP2P_E_SHAPE;
   // One item per workgroup: measured faster at the UNet's shapes than a resident grid looping over
@@ -458,7 +458,8 @@ extern "C" int vp2p_cross_attn_p2p_fwd(const vp2p_cross_attn_args* a, void* stre
     if (st % epc) return VP2P_E_ARG;
   if (a->head_dim % epc || (reinterpret_cast<uintptr_t>(a->q) & 15) || (reinterpret_cast<uintptr_t>(a->o) & 15))
     return VP2P_E_ARG;
-  const bool p2p = a->prompts > 0 && a->batch == 2 * a->prompts;
+  if (a->cond_only && !(a->prompts > 0 && a->batch == a->prompts)) return VP2P_E_ARG;
+  const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
   if (p2p && a->prompts > 4) return VP2P_E_SHAPE;
   const bool edit = p2p && (a->edit_mode != VP2P_EDIT_NONE || a->reweight);
   if (edit) {

@@ -54,11 +54,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void temporal_attn_p2p
   const int fpad = 1 << lf, G = 32 >> lf;
   const int F = a.frames, N = a.tokens;
   const int pblocks = (N + G - 1) / G;
-  const bool p2p = a.prompts > 0 && a.batch == 2 * a.prompts;
+  const bool p2p = a.prompts > 0 && a.batch == (a.cond_only ? 1 : 2) * a.prompts;
   const int RP = p2p ? a.prompts : 1;
   const int g = blockIdx.x / pblocks;
   const int pb = blockIdx.x - g * pblocks;
-  const bool replace = p2p && g == 1 && a.self_replace;
+  const bool replace = p2p && (a.cond_only || g == 1) && a.self_replace;
 
   // this lane's (token slot, frame) as a query row, and as the key row of the same index
   const int slot = r >> lf, fr = r & (fpad - 1);
@@ -206,8 +206,8 @@ static int launch_temporal(const vp2p_temporal_attn_args* a, hipStream_t s) {
   int lf = 0;
   while ((1 << lf) < a->frames) ++lf;
   const int G = 32 >> lf;
-  const bool p2p = a->prompts > 0 && a->batch == 2 * a->prompts;
-  const int groups = p2p ? 2 : a->batch;
+  const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
+  const int groups = p2p ? (a->cond_only ? 1 : 2) : a->batch;
   const int64_t nwg = (int64_t)groups * ((a->tokens + G - 1) / G);
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
   hipLaunchKernelGGL((temporal_attn_p2p_kernel<T, D>), dim3((unsigned)nwg, (unsigned)((a->heads + 3) / 4)), dim3(256),
@@ -235,7 +235,8 @@ extern "C" int vp2p_temporal_attn_p2p_fwd(const vp2p_temporal_attn_args* a, void
   for (const void* p : ptrs)
     if (reinterpret_cast<uintptr_t>(p) & 15) return VP2P_E_ARG;
   if (a->head_dim % epc) return VP2P_E_ARG;
-  if (a->self_replace && !(a->prompts > 0 && a->batch == 2 * a->prompts)) return VP2P_E_ARG;
+  if (a->cond_only && !(a->prompts > 0 && a->batch == a->prompts)) return VP2P_E_ARG;
+  if (a->self_replace && !(a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts)) return VP2P_E_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
 #define VP2P_TEMP(DIM) \
   case DIM: return a->dtype == VP2P_BF16 ? launch_temporal<bf16, DIM>(a, s) : launch_temporal<float, DIM>(a, s);

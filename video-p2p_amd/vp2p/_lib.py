@@ -89,7 +89,7 @@ class CrossAttnArgs(ctypes.Structure):
                 ("alpha_words", c_void_p), ("map_ptr", c_void_p), ("map_idx", c_void_p),
                 ("map_val", c_void_p), ("refine_alpha", c_void_p), ("equalizer", c_void_p),
                 ("lb_acc", c_void_p), ("lb_word_alpha", c_void_p), ("probs_out", c_void_p),
-                ("lb_ws", c_void_p), ("lb_sets", c_int32)]
+                ("lb_ws", c_void_p), ("lb_sets", c_int32), ("cond_only", c_int32)]
 
 
 class TemporalAttnArgs(ctypes.Structure):
@@ -100,7 +100,8 @@ class TemporalAttnArgs(ctypes.Structure):
                 ("o_sb", c_int64), ("o_sf", c_int64), ("o_sn", c_int64),
                 ("batch", c_int32), ("frames", c_int32), ("tokens", c_int32), ("heads", c_int32),
                 ("head_dim", c_int32), ("scale", c_float), ("dtype", c_int32),
-                ("prompts", c_int32), ("self_replace", c_int32), ("probs_out", c_void_p)]
+                ("prompts", c_int32), ("self_replace", c_int32), ("probs_out", c_void_p),
+                ("cond_only", c_int32)]
 
 
 class StepArgs(ctypes.Structure):

@@ -83,9 +83,18 @@ class FrameAttention(CrossAttention):
         x = hidden_states
         f = video_length
         B = x.shape[0] // f
+        shard = frame_parallel.active()
+        pending = None
+        if shard is not None and shard.world > 1 and not torch.is_grad_enabled():
+            # frames are sharded: the rank owning frame 0 broadcasts frame 0's NORMED hidden state
+            # (C per token, half the bytes of its K|V) and every rank projects K|V itself.  The
+            # broadcast is issued before this rank's Q projection so the two overlap (collective
+            # stream vs compute stream).
+            x0 = (x.view(B, f, *x.shape[1:])[:, 0].contiguous() if shard.rank == 0
+                  else torch.empty(B, *x.shape[1:], device=x.device, dtype=x.dtype))
+            pending = (x0, shard.broadcast_async(x0))
         q = F.linear(x, self.to_q.weight, self.to_q.bias)
         C = q.shape[-1]
-        shard = frame_parallel.active()
         if autograd.needs_grad(q, x):
             if shard is not None and shard.world > 1:
                 raise NotImplementedError("backward through frame-sharded FrameAttention (run null-text clip-parallel)")
@@ -94,14 +103,14 @@ class FrameAttention(CrossAttention):
                           None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
             out = autograd.SharedKVAttention.apply(q, kv, f, self.heads, self.scale)
             return self.to_out[1](self.to_out[0](out))
-        if shard is None or shard.rank == 0:   # frame 0 is local (rank 0 owns the first frames)
-            x0 = x.view(B, f, *x.shape[1:])[:, 0]
-            kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
-                          None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
+        wkv = _cat_weight(self, ("to_k", "to_v"), "_wkv")
+        bkv = None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias])
+        if pending is not None:
+            x0, work = pending
+            work.wait()
         else:
-            kv = torch.empty(B, x.shape[1], 2 * C, device=x.device, dtype=q.dtype)
-        if shard is not None:
-            kv = shard.broadcast_(kv.contiguous())
+            x0 = x.view(B, f, *x.shape[1:])[:, 0]
+        kv = F.linear(x0, wkv, bkv)
         out = ops.frame_attention(q, kv[..., :C], kv[..., C:], f, self.heads, scale=self.scale)
         return self.to_out[1](self.to_out[0](out))
 
@@ -113,6 +122,16 @@ def _batch_frames(x, controller, video_length):
     if P and x.shape[0] % (2 * P) == 0:
         return 2 * P, x.shape[0] // (2 * P), P
     return x.shape[0], 1, 0
+
+
+def _p2p_rows(B: int, P: int):
+    """(prompts, cond_only) for the attention kernels: the batch is [uncond x P, cond x P]
+    (prompts = P) -- or, on a rank of a CFG-split edit (frame_parallel.EditLayout), only the
+    unconditional rows (plain attention: prompts = 0) or only the conditional rows (cond_only)."""
+    lay = frame_parallel.active_layout()
+    if lay is not None and lay.cfg_split:
+        return (P, True) if (lay.half == 1 and P and B == P) else (0, False)
+    return (P if (P and B == 2 * P) else 0), False
 
 
 def hooked_attention(module, controller, place, x, context=None, attention_mask=None, video_length=None,
@@ -131,7 +150,7 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
     if is_cross:
         B, f, P = _batch_frames(x, controller, video_length)
         N = x.shape[1]
-        P = P if B == 2 * P else 0
+        P, cond_only = _p2p_rows(B, P)
         # the context is repeated per frame (attention.py:95); project it once per batch row
         ctx = context if context.shape[0] == B else context.reshape(B, f, *context.shape[1:])[:, 0]
         if autograd.needs_grad(x, ctx):
@@ -146,17 +165,18 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
         k = F.linear(ctx, module.to_k.weight, module.to_k.bias).contiguous()
         v = F.linear(ctx, module.to_v.weight, module.to_v.bias).contiguous()
         call = controller.fused_begin(True, place, N, f) if (controller is not None and fused) else LayerCall()
+        call.cond_only = cond_only
         probs = None
         if call.store or not fused:
             probs = torch.empty(B * f * h, N, k.shape[1], device=dev, dtype=torch.float32)
         plan = None
         lb = None
-        if fused and controller is not None and (call.edit or call.lb_acc):
+        if fused and controller is not None and P and (call.edit or call.lb_acc):
             plan = controller.plan(dev)
             if call.lb_acc:
                 lb = controller.lb_buffer(f, dev)
         out = ops.cross_attention_p2p(q, k, v, f, h, plan=plan, step=call.step, edit=call.edit, lb_acc=lb,
-                                      probs_out=probs, prompts=P, scale=module.scale)
+                                      probs_out=probs, prompts=P, scale=module.scale, cond_only=cond_only)
         if not fused:
             attn = controller(probs, True, place)
             out = _pv(module, attn, v, B, f)
@@ -193,16 +213,16 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
         P0 = getattr(controller, "batch_size", 0) or 0
         B = 2 * P0 if (P0 and x.shape[0] % (2 * P0) == 0) else 1
         N = x.shape[0] // B
-    P = getattr(controller, "batch_size", 0) or 0
-    P = P if B == 2 * P else 0
+    P, cond_only = _p2p_rows(B, getattr(controller, "batch_size", 0) or 0)
     call = controller.fused_begin(False, place, f, f) if (controller is not None and fused) else LayerCall()
+    call.cond_only = cond_only
     probs = None
     if call.store or not fused:
         probs = torch.empty(B * N * h, f, f, device=dev, dtype=torch.float32)
     replace = bool(call.self_replace) and P > 0
     if temporal_layout == "bf":
         out = ops.temporal_attention_p2p(q, k, v, f, h, prompts=P, self_replace=replace, probs_out=probs,
-                                         scale=module.scale)
+                                         scale=module.scale, cond_only=cond_only)
     else:
         out = ops.temporal_attention_p2p_bd(q, k, v, B, h, prompts=P, self_replace=replace, probs_out=probs,
                                             scale=module.scale)

@@ -53,9 +53,10 @@ class AttentionMaps(dict):
 
 class LayerCall:
     """What the fused kernel must do for one hooked layer call (built by ``fused_begin``)."""
-    __slots__ = ("edit", "step", "plan", "self_replace", "lb_acc", "store", "prompts")
+    __slots__ = ("edit", "step", "plan", "self_replace", "lb_acc", "store", "prompts", "cond_only")
 
     def __init__(self):
+        self.cond_only = False     # set by the hook: the batch is only the conditional half (CFG split)
         self.edit = False
         self.step = 0
         self.plan = None
@@ -101,10 +102,14 @@ class LocalBlend:
     def sets(self) -> int:
         return 1 if self.substruct_layers is None else 2
 
-    def advance(self, attention_store: AttentionMaps) -> Optional[torch.Tensor]:
-        """Count this step's callback (:143-144); return the LocalBlend sum if the blend fires."""
+    def advance(self, attention_store: AttentionMaps, required: bool = True) -> Optional[torch.Tensor]:
+        """Count this step's callback (:143-144); return the LocalBlend sum if the blend fires.
+        ``required=False`` (the unconditional rank of a CFG split, which never accumulates the sum):
+        return None instead of raising when there is no sum."""
         self.counter += 1
         if self.counter <= self.start_blend:
+            return None
+        if attention_store.lb_acc is None and not required:
             return None
         if attention_store.lb_acc is None:
             raise ValueError("LocalBlend has no res-16 cross-attention maps to blend with "
@@ -240,8 +245,14 @@ class AttentionStore(AttentionControl):
 
     def fused_end(self, is_cross, place_in_unet, call, probs=None):
         if call.store and probs is not None:
-            h = probs.shape[0]
-            self.step_store[f"{place_in_unet}_{'cross' if is_cross else 'self'}"].append(probs[h // 2:])
+            from . import frame_parallel
+            lay = frame_parallel.active_layout()
+            if lay is not None and lay.cfg_split and not call.cond_only:
+                pass                                   # unconditional rank of a CFG split: nothing stored
+            else:
+                h = probs.shape[0]
+                self.step_store[f"{place_in_unet}_{'cross' if is_cross else 'self'}"].append(
+                    probs if call.cond_only else probs[h // 2:])
         self._advance()
 
 
@@ -335,10 +346,7 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
 
     def lb_buffer(self, frames: int, device) -> torch.Tensor:
         st = self.attention_store
-        sets = self.local_blend.sets
-        shape = (self.batch_size, frames, LB_HW[0] * LB_HW[1])
-        if sets > 1:
-            shape = (sets,) + shape
+        shape = self.lb_shape(frames)
         if st.lb_acc is None:
             st.lb_acc = torch.zeros(shape, device=device)
             st.lb_layers_per_step = len(LB_SELECT["down"]) + len(LB_SELECT["up"])
@@ -346,11 +354,19 @@ class AttentionControlEdit(AttentionStore, abc.ABC):
             raise ValueError(f"LocalBlend sum is {tuple(st.lb_acc.shape)}, this call needs {shape}")
         return st.lb_acc
 
-    def blend_plan(self) -> Optional[torch.Tensor]:
+    def blend_plan(self, required: bool = True) -> Optional[torch.Tensor]:
         """Fused pipeline's replacement for ``step_callback``: the LocalBlend sum if it fires."""
         if self.local_blend is None:
             return None
-        return self.local_blend.advance(self.attention_store)
+        return self.local_blend.advance(self.attention_store, required)
+
+    def blend_fires(self) -> bool:
+        """Whether the NEXT step callback applies the blend (counter + 1 > start_blend, :143-144)."""
+        return self.local_blend is not None and self.local_blend.counter + 1 > self.local_blend.start_blend
+
+    def lb_shape(self, frames: int):
+        shape = (self.batch_size, frames, LB_HW[0] * LB_HW[1])
+        return shape if self.local_blend is None or self.local_blend.sets == 1 else (self.local_blend.sets,) + shape
 
     def reset(self):
         super().reset()

@@ -1,4 +1,12 @@
-"""Frame-sharded execution of one clip over G ranks; one process per GPU.
+"""Frame-sharded (and CFG-split) execution of one clip over G ranks; one process
+per GPU.
+
+``EditLayout`` decides the decomposition: with an even G >= 2 the CFG batch is split first (ranks
+[0, G/2) run the unconditional half, ranks [G/2, G) the conditional half -- both prompts, so the
+P2P source/edit pairing stays rank-local), then frames are sharded over the G/2 ranks of each half
+(``FrameShard``).  The halves meet once per denoising step, where the reference combines them
+(pipeline_tuneavideo.py:409-411, ``u + g (t - u)``): one 2-rank all-gather of the UNet outputs, plus
+a broadcast of the LocalBlend sum from the conditional rank once the blend is active.
 
 Each rank holds frames [rank*f/G, (rank+1)*f/G) of every batch row.  Only three couplings in the
 UNet cross frames, and each gets exactly one collective:
@@ -26,20 +34,37 @@ import torch
 import torch.distributed as dist
 
 _ACTIVE: Optional["FrameShard"] = None
+_LAYOUT: Optional["EditLayout"] = None
 
 
 def active() -> Optional["FrameShard"]:
+    """The frame group of the running edit (None: all frames are local)."""
     return _ACTIVE
 
 
+def active_layout() -> Optional["EditLayout"]:
+    """The full decomposition of the running edit (None: single rank / frames only)."""
+    return _LAYOUT
+
+
 @contextlib.contextmanager
-def frame_parallel(shard: Optional["FrameShard"]):
-    global _ACTIVE
-    prev, _ACTIVE = _ACTIVE, shard
+def frame_parallel(shard):
+    """Run the enclosed UNet / pipeline calls under ``shard``: a FrameShard, an EditLayout or None."""
+    global _ACTIVE, _LAYOUT
+    prev = _ACTIVE, _LAYOUT
+    if isinstance(shard, EditLayout):
+        _ACTIVE, _LAYOUT = shard.frames, shard
+    else:
+        _ACTIVE, _LAYOUT = shard, None
     try:
         yield shard
     finally:
-        _ACTIVE = prev
+        _ACTIVE, _LAYOUT = prev
+
+
+class _Done:
+    def wait(self):
+        return True
 
 
 class FrameShard:
@@ -74,6 +99,15 @@ class FrameShard:
     def broadcast_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place broadcast from group rank 0 (the owner of frame 0)."""
         return self._run(lambda x: dist.broadcast(x, src=self.src0, group=self.group), t)
+
+    def broadcast_async(self, t: torch.Tensor):
+        """Start an in-place broadcast of ``t`` from group rank 0; returns a handle whose ``wait()``
+        orders the current stream after it (RCCL: the collective runs on its own stream, so work
+        enqueued before ``wait()`` overlaps it; gloo staging completes it immediately)."""
+        if self.staged and t.is_cuda:
+            self.broadcast_(t)
+            return _Done()
+        return dist.broadcast(t, src=self.src0, group=self.group, async_op=True)
 
     def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
         if self.staged and inp.is_cuda:
@@ -135,3 +169,81 @@ class FrameShard:
         mean = s[0] / n
         var = (s[1] / n - mean * mean).clamp_min_(0.0)
         return mean, var
+
+
+def _staged_run(group, fn, t: torch.Tensor) -> torch.Tensor:
+    if dist.get_backend(group) == "gloo" and t.is_cuda:
+        h = t.detach().cpu()
+        fn(h)
+        t.copy_(h)
+        return t
+    fn(t)
+    return t
+
+
+class EditLayout:
+    """CFG split x frame sharding of one clip over all ranks of the default group.
+
+    ``half``: 0 (unconditional rows), 1 (conditional rows) or None (no CFG split: odd world or
+    ``cfg_split=False``).  ``frames``: the FrameShard of this rank's half (None when a half is one
+    rank).  Every rank creates every subgroup in the same order, as torch.distributed requires."""
+
+    def __init__(self, cfg_split: bool = True):
+        if not dist.is_initialized():
+            raise RuntimeError("EditLayout needs torch.distributed initialised (one process per GPU)")
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.cfg_split = bool(cfg_split) and self.world >= 2 and self.world % 2 == 0
+        halves = 2 if self.cfg_split else 1
+        self.frame_world = self.world // halves
+        self.half = self.rank // self.frame_world if self.cfg_split else None
+        self.frame_rank = self.rank % self.frame_world
+        fgroups = ([dist.new_group(list(range(h * self.frame_world, (h + 1) * self.frame_world)))
+                    for h in range(halves)] if self.frame_world > 1 else None)
+        pgroups = ([dist.new_group([j, j + self.frame_world]) for j in range(self.frame_world)]
+                   if self.cfg_split else None)
+        self.frames = FrameShard(fgroups[self.half or 0]) if fgroups else None
+        self.pair = pgroups[self.frame_rank] if pgroups else None
+        self.cond_src = self.frame_rank + self.frame_world       # global rank of this pair's cond half
+
+    def describe(self) -> str:
+        parts = []
+        if self.cfg_split:
+            parts.append("cfg-split x2")
+        if self.frame_world > 1:
+            parts.append(f"frame-sharded x{self.frame_world}")
+        return " x ".join(parts) or "single rank"
+
+    def frames_local(self, frames: int) -> int:
+        return self.frames.frames_local(frames) if self.frames is not None else frames
+
+    def local(self, x: torch.Tensor, dim: int = 2) -> torch.Tensor:
+        return self.frames.local(x, dim) if self.frames is not None else x
+
+    def batch_rows(self, emb: torch.Tensor) -> torch.Tensor:
+        """This rank's rows of the CFG batch [uncond x P, cond x P] (all rows without a CFG split)."""
+        if not self.cfg_split:
+            return emb
+        P = emb.shape[0] // 2
+        return emb[self.half * P:(self.half + 1) * P]
+
+    def gather_cfg(self, noise_half: torch.Tensor) -> torch.Tensor:
+        """(P, ...) UNet output of this half -> (2P, ...) [uncond, cond], identical on both ranks of
+        the pair (pipeline_tuneavideo.py:410 ``noise_pred.chunk(2)``)."""
+        if not self.cfg_split:
+            return noise_half
+        src = noise_half.contiguous()
+        staged = dist.get_backend(self.pair) == "gloo" and src.is_cuda
+        s = src.cpu() if staged else src
+        out = torch.empty((2 * s.shape[0],) + tuple(s.shape[1:]), dtype=s.dtype, device=s.device)
+        dist.all_gather_into_tensor(out, s, group=self.pair)
+        return out.to(noise_half.device)
+
+    def share_blend(self, acc: Optional[torch.Tensor], shape, device) -> torch.Tensor:
+        """The conditional rank's LocalBlend sum, on both ranks of the pair (the unconditional rank
+        never accumulates it: the controller only reads conditional maps, run_videop2p.py:217-218)."""
+        if not self.cfg_split:
+            return acc
+        if self.half == 0:
+            acc = torch.empty(shape, device=device, dtype=torch.float32)
+        buf = acc.contiguous()
+        return _staged_run(self.pair, lambda t: dist.broadcast(t, src=self.cond_src, group=self.pair), buf)

@@ -199,9 +199,10 @@ def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frame
                         plan: Optional[CrossEditPlan] = None, step: int = 0, edit: bool = True,
                         lb_acc: Optional[torch.Tensor] = None, probs_out: Optional[torch.Tensor] = None,
                         scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
-                        prompts: int = 0) -> torch.Tensor:
+                        prompts: int = 0, cond_only: bool = False) -> torch.Tensor:
     """Hooked attn2 (ptp_utils.py:196-221) with the controller edit fused.  q: (B*f, N, C);
-    k, v: the projected context (B, Nk, C) shared by all frames of a batch row."""
+    k, v: the projected context (B, Nk, C) shared by all frames of a batch row.  ``cond_only``: the
+    batch is only the conditional half (B = prompts; a CFG-split rank)."""
     dt = _dtype(q, k, v)
     Bf, N, C = q.shape
     B = Bf // frames
@@ -233,7 +234,7 @@ def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frame
                            _ptr(plan.refine_alpha) if plan is not None else None,
                            _ptr(plan.equalizer) if plan is not None else None,
                            _ptr(lb_acc), _ptr(plan.lb_word_alpha) if (plan is not None and lb_acc is not None) else None,
-                           _ptr(probs_out), None, sets)
+                           _ptr(probs_out), None, sets, int(cond_only))
     lb_ws = None
     if lb_acc is not None:       # per-head partials, reduced in head order by the library's second pass
         lb_ws = torch.empty(sets * P * heads * frames * N, device=q.device, dtype=torch.float32)
@@ -245,7 +246,7 @@ def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frame
 def temporal_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frames: int, heads: int,
                            prompts: int = 0, self_replace: bool = False,
                            probs_out: Optional[torch.Tensor] = None, scale: Optional[float] = None,
-                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                           out: Optional[torch.Tensor] = None, cond_only: bool = False) -> torch.Tensor:
     """Hooked attn_temp with replace_self_attention on '(b f) n c' tensors (B*f, N, C): the
     temporal rearrange of attention.py:263 is expressed through strides, never materialised."""
     dt = _dtype(q, k, v)
@@ -257,7 +258,7 @@ def temporal_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, fr
     d = C // heads
     a = _lib.TemporalAttnArgs(_ptr(q), _ptr(k), _ptr(v), _ptr(out), *st(q), *st(k), *st(v), *st(out),
                               B, frames, N, heads, d, float(d ** -0.5 if scale is None else scale), dt,
-                              prompts, int(self_replace), _ptr(probs_out))
+                              prompts, int(self_replace), _ptr(probs_out), int(cond_only))
     check(_lib.load().vp2p_temporal_attn_p2p_fwd(ctypes.byref(a), _stream()), "vp2p_temporal_attn_p2p_fwd")
     return out
 

@@ -18,7 +18,7 @@ from typing import List, Optional, Union
 
 import torch
 
-from . import ops
+from . import frame_parallel, ops
 from .attention import register_attention_control
 from .scheduler import DDIMScheduler
 
@@ -77,13 +77,30 @@ class VideoP2PPipeline:
         lb_th = (0.3, 0.3)
         if fused and controller.local_blend is not None:
             lb_th = controller.local_blend.th
+        # CFG split (frame_parallel.EditLayout): this rank runs one half of the CFG batch; the halves
+        # meet in one all-gather of the UNet output per step, exactly where the reference combines them
+        lay = frame_parallel.active_layout()
+        split = lay is not None and lay.cfg_split
+        if split and not (fused or controller is None):
+            raise NotImplementedError("a CFG-split edit needs a vp2p controller (fused protocol)")
         for i, t in enumerate(self.scheduler.timesteps.tolist()):
             if uncond_embeddings_pre is not None:
                 emb[0] = uncond_embeddings_pre[i]
-            model_in = torch.cat([lat, lat])
-            noise = self.unet(model_in, t, encoder_hidden_states=emb).sample.contiguous()
+            if split:
+                noise = self.unet(lat, t, encoder_hidden_states=lay.batch_rows(emb)).sample
+                noise = lay.gather_cfg(noise)
+            else:
+                model_in = torch.cat([lat, lat])
+                noise = self.unet(model_in, t, encoder_hidden_states=emb).sample.contiguous()
             if fused or controller is None:
-                acc = controller.blend_plan() if fused else None
+                acc = None
+                if fused and split:
+                    fires = controller.blend_fires()
+                    acc = controller.blend_plan(required=lay.half == 1)
+                    if fires:
+                        acc = lay.share_blend(acc, controller.lb_shape(lat.shape[2]), dev)
+                elif fused:
+                    acc = controller.blend_plan()
                 lat = ops.step_fused(noise, lat, self.scheduler.step_constants(t), guidance_scale, cfg=True,
                                      fast=fast, lb_acc=acc, lb_count=40.0, lb_th=lb_th[0], lb_sub_th=lb_th[1])
             else:  # foreign controller: reference order, step_callback on the new latents
