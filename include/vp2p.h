@@ -43,7 +43,7 @@ enum vp2p_status {
   VP2P_E_ARG = -1,        /* null pointer / negative size / inconsistent sizes */
   VP2P_E_DTYPE = -2,      /* dtype not supported by this entry point */
   VP2P_E_HEAD_DIM = -3,   /* head_dim without a compiled kernel instance */
-  VP2P_E_SHAPE = -4,      /* size above a kernel limit (frames > 32 temporal, tokens_kv > 128 cross) */
+  VP2P_E_SHAPE = -4,      /* size above a kernel limit (frames > 128 temporal, tokens_kv > 128 cross) */
   VP2P_E_LAUNCH = -5      /* hipLaunchKernelGGL reported an error */
 };
 
@@ -143,7 +143,7 @@ int vp2p_cross_kv_prep(const void* k, const void* v, int64_t k_sb, int64_t k_sn,
 
 int vp2p_cross_attn_p2p_fwd(const vp2p_cross_attn_args* args, void* stream);
 
-/* ---- K3: hooked temporal attention (frames <= 32) + self-attention replace -------------------- */
+/* ---- K3: hooked temporal attention (frames <= 128) + self-attention replace ------------------- */
 typedef struct vp2p_temporal_attn_args {
   const void* q; const void* k; const void* v; void* o;   /* (batch, frames, tokens, C) strided */
   int64_t q_sb, q_sf, q_sn;

@@ -180,7 +180,8 @@ def test_cross_attention_plain(dtype):
 
 # ------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("frames,d,step", [(8, 40, 0), (8, 40, 30), (24, 80, 3), (3, 160, 1), (16, 40, 0)])
+@pytest.mark.parametrize("frames,d,step", [(8, 40, 0), (8, 40, 30), (24, 80, 3), (3, 160, 1), (16, 40, 0),
+                                           (48, 40, 0), (128, 80, 3), (64, 160, 1), (33, 32, 30)])
 def test_temporal_attention_p2p(tokenizer, dtype, frames, d, step):
     from vp2p import ops
     heads, P, n = 8, 2, 48

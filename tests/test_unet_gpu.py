@@ -98,3 +98,34 @@ def test_edit_loop_fast_mode(tokenizer, substruct):
         eps = unet_ref.unet_forward(sd, torch.from_numpy(np.concatenate([lat, lat])), int(t), ctx, octrl).numpy()
         lat = octrl.step_callback(d.step(O.cfg(eps, 7.5, True), int(t), lat))
     assert np.abs(got - lat).max() / np.abs(lat).max() < 1e-3
+
+
+@pytest.mark.parametrize("frames", [40, 128])
+def test_transformer_long_clip(tokenizer, frames):
+    """A Transformer3DModel over a long clip (f > 32: the K3 long-clip kernel behind attn_temp, with
+    the self-replace active) vs the oracle transformer (oracle/unet_ref.py, pinned to the reference's
+    attention.py) with the oracle controller."""
+    import vp2p
+    from vp2p.unet3d import Transformer3DModel, init_random_
+    prompts, swap, blend, eq, cross, self_ = spec.CONFIGS["rabbit"]
+    C, h, w = 320, 4, 4
+    m = init_random_(Transformer3DModel(8, C // 8, C, 64), seed=5, std=0.05)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.cuda().to(memory_format=torch.channels_last)
+    ctrl = vp2p.make_controller(prompts, swap, {"default_": cross}, self_, None, eq, tokenizer=tokenizer)
+    octrl = O.EditController(prompts, swap, {"default_": cross}, self_, tokenizer, eq_params=eq)
+    holder = torch.nn.Module()
+    holder.down_blocks = m                       # registration walks the down*/mid*/up* children
+    vp2p.register_attention_control(type("M", (), {"unet": holder})(), ctrl)
+    assert ctrl.num_att_layers == 2
+    octrl.num_att_layers = 2
+    g = np.random.default_rng(9)
+    x5 = torch.from_numpy(g.standard_normal((4, C, frames, h, w)).astype(np.float32))
+    ctx = torch.from_numpy(g.standard_normal((4, 77, 64)).astype(np.float32))
+    ctx[:2] = ctx[0]
+    xb = x5.permute(0, 2, 1, 3, 4).reshape(4 * frames, C, h, w).cuda().contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        got = m(xb, ctx.cuda(), frames).reshape(4, frames, C, h, w).permute(0, 2, 1, 3, 4).cpu()
+        ref = unet_ref.transformer(sd, "", x5, ctx, octrl, "down")
+    assert ctrl.self_replace_active(frames)
+    assert _rel(got, ref) < 2e-4, _rel(got, ref)

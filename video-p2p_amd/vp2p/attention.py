@@ -239,8 +239,8 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
 def _out_proj(to_out, out, residual):
     """``to_out(out)``, plus ``residual`` when the caller passes the block's residual
     (``attn_temp(norm_temp(x)) + x``, attention.py:268).  At inference the add runs in the epilogue
-    of K10's GEMM core when that measured faster for the shape than hipBLASLt + a separate add
-    (``ops.CONV.pick``, the same per-shape choice as the proj_out fusion)."""
+    of K10's GEMM core when the in-tree kernel-choice table says it is faster for the shape than
+    hipBLASLt + a separate add (``ops.CONV.pick``, the same per-shape choice as the proj_out fusion)."""
     if residual is None:
         return to_out(out)
     if torch.is_grad_enabled() or not isinstance(to_out, nn.Linear) or not out.is_contiguous() \
@@ -254,7 +254,7 @@ def _out_proj(to_out, out, residual):
     def lib():
         return to_out(out) + res
 
-    key = ("to_out_res", tuple(out.shape), tuple(to_out.weight.shape), out.device.index)
+    key = ("to_out_res", tuple(out.shape), tuple(to_out.weight.shape))
     ok = ops.linear_residual_supported(out, to_out.weight, res)
     return fused() if ops.CONV.pick(key, ok, fused, lib) else lib()
 

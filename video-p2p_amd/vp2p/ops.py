@@ -9,6 +9,8 @@ there is no CPU path.  Shapes follow the reference's tensors:
 from __future__ import annotations
 
 import ctypes
+import json
+import os
 from typing import Optional
 
 import torch
@@ -558,22 +560,43 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
 
 class ConvSelector:
     """Per-shape choice between a K10 launch and the library path (MIOpen convolution, hipBLASLt
-    GEMM + K9), measured on the device the first time a shape is seen (a few launches of each,
-    timed with HIP events; the one sync happens at that first call only, i.e. during warmup) and
-    cached for the process."""
+    GEMM + K9 / a separate add).
+
+    The choice is read from an in-tree table (``miopen_db/kernel_choices.json``), measured once on
+    the MI355X by ``tools/choose_kernels.py`` for every shape the pipeline, the inversion, the
+    null-text loop and the multi-GPU layouts run.  K10 and the library are not bit-equal, so a
+    fixed table keeps the numerics identical from run to run, box to box and rank to rank (a
+    per-process timing race would not).  Shapes missing from the table take a fixed rule: K10
+    wherever it covers the shape.  ``VP2P_CONV``: ``table`` (default) | ``k10`` | ``library`` |
+    ``tune`` (time both on first use -- the mode the table is generated in)."""
+
+    TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                         "miopen_db", "kernel_choices.json")
 
     def __init__(self):
+        self.mode = os.environ.get("VP2P_CONV", "table")
+        if self.mode not in ("table", "k10", "library", "tune"):
+            raise ValueError(f"VP2P_CONV={self.mode!r}: expected table | k10 | library | tune")
+        self.table = {}
+        if os.path.exists(self.TABLE):
+            with open(self.TABLE) as fh:
+                self.table = {k: bool(v) for k, v in json.load(fh)["choices"].items()}
         self.choice = {}
-        # VP2P_CONV=library | k10 | auto (default): A/B switch for experiments
-        import os
-        self.mode = os.environ.get("VP2P_CONV", "auto")
+
+    @staticmethod
+    def key_str(key) -> str:
+        return "|".join(str(k) for k in key)
 
     def pick(self, key, supported: bool, k10, library) -> bool:
-        use = self.choice.get(key)
+        if not supported or self.mode == "library":
+            return False
+        if self.mode == "k10":
+            return True
+        ks = self.key_str(key)
+        use = self.choice.get(ks)
         if use is None:
-            ok = self.mode != "library" and supported
-            use = ok and (self.mode == "k10" or self._faster(k10, library))
-            self.choice[key] = use
+            use = self._faster(k10, library) if self.mode == "tune" else self.table.get(ks, True)
+            self.choice[ks] = use
         return use
 
     def run(self, x, weight, bias, stride: int, padding: int, residual, library, upsample: bool = False):
@@ -584,8 +607,7 @@ class ConvSelector:
             y = library()
             return y if residual is None else residual + y
 
-        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, residual is not None, upsample,
-               x.device.index)
+        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, residual is not None, upsample)
         if self.pick(key, conv2d_supported(x, weight, stride, padding, upsample), k10, lib):
             return k10()
         return lib()

@@ -109,8 +109,8 @@ class InflatedConv3d(nn.Conv2d):
     """Per-frame Conv2d (resnet.py:11-19); input/output already '(b f) c h w' channels-last.
 
     Runs on K10 (``ops.conv2d``, implicit GEMM with the bias and an optional residual add fused) or
-    on MIOpen, whichever ``ops.ConvSelector`` measured faster for this shape on this GPU; the choice
-    is made once per shape (first call) and cached.  ``residual``: added to the output (the resnet
+    on MIOpen, per the in-tree per-shape choice table (``ops.ConvSelector``; measured offline on the
+    MI355X, so every run and every rank takes the same numerics).  ``residual``: added to the output (the resnet
     shortcut add, fused on K10)."""
 
     def forward(self, x, residual: Optional[torch.Tensor] = None):
@@ -163,7 +163,7 @@ class GEGLU(nn.Module):
             return ops.linear_geglu(x, *self._interleaved())
 
         # measured per shape: K10 wins where K is small (res-64, K = 320), hipBLASLt's GEMM elsewhere
-        key = ("geglu", tuple(x.shape), tuple(self.proj.weight.shape), x.device.index)
+        key = ("geglu", tuple(x.shape), tuple(self.proj.weight.shape))
         ok = _FUSE_GEGLU and ops.linear_geglu_supported(x, self.proj.weight)
         return fused() if ops.CONV.pick(key, ok, fused, unfused) else unfused()
 
@@ -250,7 +250,7 @@ class Transformer3DModel(nn.Module):
             def lib():
                 return F.linear(tok, w_out, self.proj_out.bias) + res
 
-            key = ("proj_out", tuple(tok.shape), tuple(w_out.shape), x.device.index)
+            key = ("proj_out", tuple(tok.shape), tuple(w_out.shape))
             ok = ops.linear_residual_supported(tok, w_out, res)
             out = fused() if ops.CONV.pick(key, ok, fused, lib) else lib()
             return out.reshape(Bf, H, W, C).permute(0, 3, 1, 2)
