@@ -29,14 +29,21 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "miopen_db", "kernel_choices.json"))
     ap.add_argument("--cases", default=",".join(f"{b}x{f}" for b, f in CASES))
     args = ap.parse_args()
+    t0 = time.time()
     from vp2p import ops
     from vp2p.tuning import use_tuned_libraries
     from vp2p.unet3d import UNet3DConditionModel, init_random_
     use_tuned_libraries()
+    import threading
+
+    def beat():          # new conv shapes compile MIOpen kernels for minutes: keep the run visibly alive
+        while True:
+            time.sleep(30)
+            print(f"[choose] ... {len(ops.CONV.choice)} shapes ({time.time() - t0:.0f} s)", flush=True)
+    threading.Thread(target=beat, daemon=True).start()
     dev = torch.device("cuda")
     unet = init_random_(UNet3DConditionModel(), seed=0).to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
     unet.eval()
-    t0 = time.time()
     with torch.no_grad():
         for case in args.cases.split(","):
             B, f = (int(v) for v in case.split("x"))

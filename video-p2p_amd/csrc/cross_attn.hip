@@ -19,6 +19,10 @@
 // edit is a handful of LDS reads per word and nothing but Q in / O out touches HBM.
 // The 77-token K/V (identical for all frames: attention.py:95 repeats the context per frame) are
 // pre-laid-out once per layer by vp2p_cross_kv_prep into MFMA fragment order and read through L1/L2.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "common.hpp"
 #include "vp2p.h"
 
@@ -324,6 +328,235 @@ void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// K2 v2 (bf16, d <= 64, two prompts): K/V live in REGISTERS, waves are persistent.
+//
+// The 77-key K/V of one (batch row, head) is the same for every query block, so each wave loads its
+// row's K fragments (KB x KS) and V^T fragments (NT x KB x 2) once and then streams query blocks:
+// per block only Q (prefetched one block ahead) comes in and O goes out -- the HBM traffic the
+// roofline counts -- with no K/V re-reads through L2 per block (the v1 kernel's 21 KB per wave and
+// prompt) and no per-block dependency on a K/V fetch.
+// Waves pair up on the prompts of one CFG half: wave 2s+p runs prompt p of query stream s.  In the
+// conditional half the source wave (p = 0) parks its probabilities in an LDS ring (two slots per
+// pair) and the edited wave (p = 1) reads them after one workgroup barrier per block (run_videop2p.py
+// :304-317); the unconditional half / plain batches need no exchange.
+// ------------------------------------------------------------------------------------------------
+template <int D, int KB>
+__global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_attn_args a, int prow, int iters) {
+  using T = bf16;
+  using M = Mfma<T>;
+  using C = CrossCfg<T, D>;
+  constexpr int KP = 32 * KB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int FQ = a.frames * a.tokens_q;
+  const int qblocks = (FQ + 31) >> 5;
+  const bool p2p = a.prompts == 2 && a.batch == (a.cond_only ? 1 : 2) * a.prompts;
+  const int g = blockIdx.y;                    // CFG half (p2p) or batch row
+  const int head = blockIdx.z;
+  const bool cond = p2p && (a.cond_only || g == 1);
+  const bool edit = cond && (a.edit_mode != VP2P_EDIT_NONE || a.reweight);
+  const bool lb = cond && a.lb_acc != nullptr;
+  const int NKV = a.tokens_kv;
+  // wave roles: p2p -> (prompt, stream) = (w & 1, w >> 1), 2 streams; plain -> prompt 0, 4 streams
+  const int pw = p2p ? (w & 1) : 0;
+  const int sw = p2p ? (w >> 1) : w;
+  const int NS = p2p ? 2 : 4;
+  const int b = p2p ? g * 2 + pw : g;          // batch row of this wave
+
+  float* ring = reinterpret_cast<float*>(smem);                      // [2 streams][2 slots][32][prow]
+  f32x4* etab = reinterpret_cast<f32x4*>(ring + 2 * 2 * 32 * prow);  // [NKV] (one edited prompt)
+  float* lbw = reinterpret_cast<float*>(etab + NKV);                  // [sets][2][NKV]
+  const int LBS = a.lb_sets == 2 ? 2 : 1;
+  if (edit) {
+    for (int i = tid; i < NKV; i += 256) {
+      f32x4 t;
+      t[0] = a.edit_mode == VP2P_EDIT_REFINE ? a.refine_alpha[i] : 0.f;
+      t[1] = a.reweight ? a.equalizer[i] : 1.f;
+      t[2] = a.alpha_words[i];
+      t[3] = __int_as_float(a.edit_mode == VP2P_EDIT_REFINE ? a.map_idx[i] : i);
+      etab[i] = t;
+    }
+  }
+  if (lb)
+    for (int i = tid; i < LBS * 2 * NKV; i += 256) lbw[i] = a.lb_word_alpha[i];
+  __syncthreads();
+
+  // this wave's K (A fragments of S^T) and V^T (A fragments of O^T), resident for the whole loop
+  const T* ws = static_cast<const T*>(a.kv_ws);
+  const int64_t kelems = (int64_t)a.batch * a.heads * KP * C::DP;
+  const T* kb_base = ws + ((int64_t)(b * a.heads + head) * KP) * C::DP;
+  const T* vb_base = ws + kelems + ((int64_t)(b * a.heads + head) * KP) * C::DV;
+  bf16x8 kf[KB][C::KS], vf[KB][2][C::NT];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s)
+      kf[kb][s] = *reinterpret_cast<const bf16x8*>(kb_base + (kb * 32 + r) * C::DP + 16 * s + 8 * h);
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t)
+        vf[kb][sp][t] = *reinterpret_cast<const bf16x8*>(vb_base + (int64_t)(32 * t + r) * KP + kb * 32 + 16 * sp + 8 * h);
+  }
+
+  const float cs = a.scale * kLog2e;
+  const int qb0 = blockIdx.x * NS * iters + sw;    // this stream's blocks: qb0, qb0 + NS, ...
+  auto load_q = [&](int qb, bf16x8* dst) {
+    const int qi = qb * 32 + r;
+    const bool ok = qb < qblocks && qi < FQ;
+    const int fr = ok ? qi / a.tokens_q : 0;
+    const int pos = ok ? qi - fr * a.tokens_q : 0;
+    const T* row = static_cast<const T*>(a.q) + b * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * D;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) dst[s] = ok ? M::row_frag(row, s, h, D) : M::zero();
+  };
+  bf16x8 qn[C::KS];
+  load_q(qb0, qn);
+
+  for (int it = 0; it < iters; ++it) {
+    const int qb = qb0 + it * NS;
+    bf16x8 qf[C::KS];
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[s] = qn[s];
+    if (it + 1 < iters) load_q(qb + NS, qn);
+    const int qi = qb * 32 + r;
+    const bool qv = qb < qblocks && qi < FQ;
+    const int fr = qv ? qi / a.tokens_q : 0;
+    const int pos = qv ? qi - fr * a.tokens_q : 0;
+
+    f32x16 sc[KB];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      sc[kb] = zero16();
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) sc[kb] = M::mma(kf[kb][s], qf[s], sc[kb]);
+    }
+    // row softmax: only the last key block is ragged (keys >= NKV masked); max on raw scores,
+    // exp2(s * cs - max * cs) as one fma
+    float mx = kNegInf;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (kb == KB - 1 && kb * 32 + acc_row(i, h) >= NKV) sc[kb][i] = kNegInf;
+        mx = fmaxf(mx, sc[kb][i]);
+      }
+    mx = fmaxf(mx, xhalf(mx)) * cs;
+    float sum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = fast_exp2(__builtin_fmaf(sc[kb][i], cs, -mx));
+        sc[kb][i] = e;
+        sum += e;
+      }
+    sum += xhalf(sum);
+    const float inv = 1.f / sum;
+    // probabilities are read (edit, LocalBlend sum, stored maps): normalise them; otherwise 1/sum is
+    // applied to O at the end (flash-style; the same softmax, fewer VALU ops per score)
+    const bool norm_p = edit || lb || a.probs_out;
+    if (norm_p) {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[kb][i] *= inv;
+    }
+    const float oscale = norm_p ? 1.f : inv;
+
+    if (edit) {
+      float* slot = ring + ((sw * 2 + (it & 1)) * 32 + r) * prow;
+      if (pw == 0) {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) slot[wd] = sc[kb][i];
+          }
+      }
+      __syncthreads();                         // source probabilities of this block are parked
+      if (pw == 1) {
+#pragma clang fp contract(off)
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) {
+              const float pe_val = sc[kb][i];
+              const f32x4 t = etab[wd];
+              float R;
+              if (a.edit_mode == VP2P_EDIT_REPLACE) {
+                float gsum = 0.f;
+                for (int n = a.map_ptr[wd]; n < a.map_ptr[wd + 1]; ++n) gsum += slot[a.map_idx[n]] * a.map_val[n];
+                R = gsum;
+              } else if (a.edit_mode == VP2P_EDIT_REFINE) {
+                R = slot[__float_as_int(t[3])] * t[0] + pe_val * (1.f - t[0]);
+              } else {
+                R = slot[wd];
+              }
+              R = R * t[1];
+              sc[kb][i] = R * t[2] + (1.f - t[2]) * pe_val;
+            }
+          }
+      }
+    }
+    if (lb) {  // this head's word-weighted map of token qi -> lb_ws[set][p][head][qi]
+      for (int set = 0; set < LBS; ++set) {
+        const float* wts = lbw + (set * 2 + pw) * NKV;
+        float part = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) part += wts[wd] * sc[kb][i];
+          }
+        part += xhalf(part);
+        if (h == 0 && qv) a.lb_ws[((int64_t)(set * 2 + pw) * a.heads + head) * FQ + qi] = part;
+      }
+    }
+    if (a.probs_out && qv) {
+      float* prow_out = a.probs_out + ((((int64_t)b * a.frames + fr) * a.heads + head) * a.tokens_q + pos) * NKV;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int wd = kb * 32 + acc_row(i, h);
+          if (wd < NKV) prow_out[wd] = sc[kb][i];
+        }
+    }
+    f32x16 o[C::NT];
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t) o[t] = zero16();
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        const bf16x8 pf = M::p_frag(sc[kb], sp);
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t) o[t] = M::mma(vf[kb][sp][t], pf, o[t]);
+      }
+    if (qv) {
+      T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int dc = 32 * t + 8 * gq + 4 * h;
+          if (dc < D) {
+            bf16x4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[t][4 * gq + j] * oscale);
+            *reinterpret_cast<bf16x4*>(orow + dc) = v;
+          }
+        }
+    }
+  }
+}
+
 // lb_acc[p][qi] += sum over heads (in head order) of lb_ws[p][head][qi]: deterministic, one
 // read-modify-write per (prompt, token).
 __global__ void cross_lb_reduce_kernel(float* __restrict__ lb_acc, const float* __restrict__ lb_ws,
@@ -356,9 +589,51 @@ static int cross_pad_dims(int head_dim, int dtype, int& dp, int& dv) {
 #undef VP2P_DIMS
 }
 
+static int cross_v2_disabled() {   // VP2P_K2=v1: A/B switch, read once
+  static const int off = [] {
+    const char* e = getenv("VP2P_K2");
+    return (e && e[0] == 'v' && e[1] == '1') ? 1 : 0;
+  }();
+  return off;
+}
+
 template <typename T, int D, int KB>
 static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
   const int FQ = a->frames * a->tokens_q;
+  if constexpr (sizeof(T) == 2 && D <= 64) {
+    const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
+    // edit launches (the first int(cross_replace * 51) steps) keep v1: its one-wave-per-item walk over
+    // both prompts needs no cross-wave exchange of the source probabilities (v2's pair barrier
+    // measured slower there: 163 vs 129 us at res-64)
+    const bool edit = p2p && (a->edit_mode != VP2P_EDIT_NONE || a->reweight);
+    if ((!p2p || a->prompts == 2) && !edit && !cross_v2_disabled()) {
+      const int groups = p2p ? (a->cond_only ? 1 : 2) : a->batch;
+      const int NS = p2p ? 2 : 4;
+      const int64_t qblocks = (FQ + 31) / 32;
+      const int64_t per_group = (qblocks + NS - 1) / NS;          // iterations of one stream, all blocks
+      // enough workgroups for ~2 per CU over the (group, head) grid; each stream then loops `iters`
+      const int64_t gh = (int64_t)groups * a->heads;
+      int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_group, (512 + gh - 1) / gh));
+      const int iters = (int)((per_group + nx - 1) / nx);
+      nx = (per_group + iters - 1) / iters;
+      if (gh > 65535 * 64 || nx > 0x7fffffff) return VP2P_E_SHAPE;
+      const int prow = a->tokens_kv | 1;
+      const int sets = a->lb_sets == 2 ? 2 : 1;
+      const size_t lds = (size_t)2 * 2 * 32 * prow * sizeof(float) + (size_t)a->tokens_kv * 16 +
+                         (size_t)sets * 2 * a->tokens_kv * sizeof(float);
+      hipLaunchKernelGGL((cross_attn_kernel_v2<D, KB>), dim3((unsigned)nx, (unsigned)groups, (unsigned)a->heads),
+                         dim3(256), lds, s, *a, prow, iters);
+      if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
+      if (p2p && a->lb_acc) {
+        const int64_t n = (int64_t)sets * a->prompts * FQ;
+        const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(cross_lb_reduce_kernel, dim3(blocks), dim3(256), 0, s, a->lb_acc, a->lb_ws,
+                           sets * a->prompts, a->heads, FQ);
+        if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
+      }
+      return VP2P_OK;
+    }
+  }
   const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
   const int groups = p2p ? (a->cond_only ? 1 : 2) : a->batch;
   const int64_t items = (int64_t)((FQ + 31) / 32) * ((a->heads + 3) / 4);

@@ -22,10 +22,9 @@
 //      - masking only on the ragged last tile.
 //  * next K/V tile prefetched into registers while the current one is consumed
 //    (issue early / write late); two barriers per 128-key tile.
-//  * bf16, d <= 64 (the res-64 layers, 88% of the FLOPs): frame_attn_kernel_x2 gives every wave
-//    64 query rows as two independent 32-row sets sharing each K/V fragment read (half the LDS
-//    traffic per query, two independent MFMA/VALU chains per wave): +5% over one set per wave in
-//    an interleaved A/B (profiles/r01_k1_ab.txt).
+//  * bf16, d <= 80 (the res-64 and res-32 layers, 98% of the FLOPs): frame_attn_kernel_x2f gives
+//    every wave 64 query rows as two independent 32-row sets sharing each K/V fragment read (half
+//    the LDS traffic per query, two independent MFMA/VALU chains per wave) -- see its header.
 #include <stdlib.h>
 
 #include <type_traits>
@@ -269,180 +268,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
   }
 }
 
-// Variant with 64 query rows per wave: two independent 32-row sets share every K/V fragment read
-// (half the LDS traffic per query) and give the scheduler two independent MFMA/VALU chains.
-// bf16, head dims with a spare ones row (d = 32 excluded), d <= 64.
-template <int D>
-__global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2(const vp2p_frame_attn_args a) {
-  using T = bf16;
-  using M = Mfma<T>;
-  using C = FrameCfg<T, D>;
-  static_assert(C::ONES && D <= 64, "x2 variant: bf16, spare ones row");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* Ks = reinterpret_cast<T*>(smem);
-  T* Vs = Ks + C::KT * C::KROW;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
-  const int FQ = a.frames * a.tokens_q;
-  const int qblocks = (FQ + 255) >> 8;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = bid / qblocks, qb = bid - bh * qblocks;
-  const int b = bh / a.heads, head = bh - b * a.heads;
-  const int Nk = a.tokens_kv;
-
-  int qi[2], fr[2], pos[2];
-  bool qv[2];
-  bf16x8 qf[2][C::KS];
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    qi[st] = qb * 256 + w * 64 + st * 32 + r;
-    qv[st] = qi[st] < FQ;
-    fr[st] = qv[st] ? qi[st] / a.tokens_q : 0;
-    pos[st] = qv[st] ? qi[st] - fr[st] * a.tokens_q : 0;
-    const T* qrow = static_cast<const T*>(a.q) + b * a.q_sb + fr[st] * a.q_sf + pos[st] * a.q_sn + head * D;
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) qf[st][s] = qv[st] ? M::row_frag(qrow, s, h, D) : M::zero();
-  }
-  for (int i = tid; i < C::LDS_BYTES / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0, 0, 0, 0};
-  __syncthreads();
-  for (int k = tid; k < C::KT; k += 256) Vs[k * C::VROW + D] = (T)1.0f;
-
-  const T* kbase = static_cast<const T*>(a.k) + b * a.k_sb + head * D;
-  const T* vbase = static_cast<const T*>(a.v) + b * a.v_sb + head * D;
-  u32x4 kreg[C::NCH], vreg[C::NCH];
-  auto load_tile = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < C::NCH; ++i) {
-      const int c = tid + i * 256;
-      const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
-      const int key = kt + row;
-      if (c < C::KT * C::CPR && key < Nk) {
-        kreg[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)key * a.k_sn + col);
-        vreg[i] = *reinterpret_cast<const u32x4*>(vbase + (int64_t)key * a.v_sn + col);
-      } else {
-        kreg[i] = u32x4{0, 0, 0, 0};
-        vreg[i] = u32x4{0, 0, 0, 0};
-      }
-    }
-  };
-  auto store_tile = [&]() {
-#pragma unroll
-    for (int i = 0; i < C::NCH; ++i) {
-      const int c = tid + i * 256;
-      if (c < C::KT * C::CPR) {
-        const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
-        *reinterpret_cast<u32x4*>(Ks + row * C::KROW + col) = kreg[i];
-        *reinterpret_cast<u32x4*>(Vs + row * C::VROW + col) = vreg[i];
-      }
-    }
-  };
-
-  const float cs = a.scale * kLog2e;
-  float m[2] = {kNegInf, kNegInf};
-  f32x16 o[2][C::NT];
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int t = 0; t < C::NT; ++t) o[st][t] = zero16();
-
-  auto compute_tile = [&](int kt, auto masked_tag) {
-    constexpr bool MASKED = decltype(masked_tag)::value;
-#pragma unroll
-    for (int key0 = 0; key0 < C::KT; key0 += 32) {
-      if (MASKED && kt + key0 >= Nk) break;
-      f32x16 s[2] = {zero16(), zero16()};
-#pragma unroll
-      for (int si = 0; si < C::KS; ++si) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ks + (key0 + r) * C::KROW + 16 * si + 8 * h);
-        s[0] = M::mma(af, qf[0][si], s[0]);
-        s[1] = M::mma(af, qf[1][si], s[1]);
-      }
-      float mx[2];
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        if constexpr (MASKED) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i)
-            if (kt + key0 + acc_row(i, h) >= Nk) s[st][i] = kNegInf;
-        }
-        float v = s[st][0];
-#pragma unroll
-        for (int i = 1; i < 16; ++i) v = fmaxf(v, s[st][i]);
-        mx[st] = fmaxf(v, xhalf(v)) * cs;
-      }
-      if (__any(mx[0] > m[0] + kRescaleThr || mx[1] > m[1] + kRescaleThr)) {
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const float mn = fmaxf(m[st], mx[st]);
-          const float alpha = fast_exp2(m[st] - mn);
-          m[st] = mn;
-#pragma unroll
-          for (int t = 0; t < C::NT; ++t)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) o[st][t][i] *= alpha;
-        }
-      }
-      bf16x8 pf[2][2];
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const float nm = -m[st];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[st][i] = fast_exp2(__builtin_fmaf(s[st][i], cs, nm));
-        pf[st][0] = M::p_frag(s[st], 0);
-        pf[st][1] = M::p_frag(s[st], 1);
-      }
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp)
-#pragma unroll
-        for (int t = 0; t < C::NT; ++t) {
-          const bf16x8 vf = vt_frag_lds<C::VROW>(Vs, key0, sp, t);
-          o[0][t] = M::mma(vf, pf[0][sp], o[0][t]);
-          o[1][t] = M::mma(vf, pf[1][sp], o[1][t]);
-        }
-    }
-  };
-
-  load_tile(0);
-  int kt = 0;
-  for (; kt + C::KT <= Nk; kt += C::KT) {
-    __syncthreads();
-    store_tile();
-    __syncthreads();
-    if (kt + C::KT < Nk) load_tile(kt + C::KT);
-    compute_tile(kt, std::false_type{});
-  }
-  if (kt < Nk) {
-    __syncthreads();
-    store_tile();
-    __syncthreads();
-    compute_tile(kt, std::true_type{});
-  }
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    const float mine = o[st][C::ONE_T][C::ONE_I];
-    const float other = xhalf(mine);
-    const float lrow = (h == C::ONE_H) ? mine : other;
-    if (a.lse && qv[st]) a.lse[(int64_t)(b * a.heads + head) * FQ + qi[st]] = m[st] + log2f(lrow);
-    if (qv[st]) {
-      const float inv = 1.f / lrow;
-      T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr[st] * a.o_sf + pos[st] * a.o_sn + head * D;
-#pragma unroll
-      for (int t = 0; t < C::NT; ++t)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int dc = 32 * t + 8 * g + 4 * h;
-          if (dc < D) {
-            bf16x4 v;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[st][t][4 * g + j] * inv);
-            *reinterpret_cast<bf16x4*>(orow + dc) = v;
-          }
-        }
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
-// x2f: bf16, d <= 64 with a spare V^T row (d = 40, the res-64 layers, 88% of the FLOPs).
+// x2f: bf16, d <= 80 with a spare V^T row (d = 40: the res-64 layers, 88% of the FLOPs, 256-key
+// tiles; d = 80: the res-32 layers, 64-key tiles to stay within the register budget).
 // frame_attn_kernel_x2 with the inner 128-key tile made one straight-line, software-pipelined block:
 //  * no per-score max: m starts at the exact row max of the first 32-key block; afterwards growth
 //    is read off the ones-row sum (O^T row D) once per tile: if the tile's sum dl = l - l_prev
@@ -458,45 +286,40 @@ constexpr float kSumThr = 4096.f;
 
 // Exact two-pass softmax row of one query in plain fp32 VALU (the overflow fallback of x2f):
 // writes this lane's epilogue slots of the output row and the row's log-sum-exp.
+// Small register footprint (the query row is re-read from memory, one 4-column output slot
+// accumulated at a time) so this rare path does not add to the kernel's register budget.
 template <int D>
 __device__ __forceinline__ void frame_attn_exact_row(const vp2p_frame_attn_args& a, int b, int head, int fr,
                                                      int pos, int64_t qi, int h, float cs) {
   const bf16* qrow = static_cast<const bf16*>(a.q) + b * a.q_sb + (int64_t)fr * a.q_sf + (int64_t)pos * a.q_sn + head * D;
   const bf16* kb = static_cast<const bf16*>(a.k) + b * a.k_sb + head * D;
   const bf16* vb = static_cast<const bf16*>(a.v) + b * a.v_sb + head * D;
-  float qv[D], acc[D];
-#pragma unroll
-  for (int c = 0; c < D; ++c) { qv[c] = (float)qrow[c]; acc[c] = 0.f; }
+  auto score = [&](int key) {
+    const bf16* kr = kb + (int64_t)key * a.k_sn;
+    float s = 0.f;
+    for (int c = 0; c < D; ++c) s = __builtin_fmaf((float)qrow[c], (float)kr[c], s);
+    return s;
+  };
   float mx = kNegInf;
-  for (int key = 0; key < a.tokens_kv; ++key) {
-    const bf16* kr = kb + (int64_t)key * a.k_sn;
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < D; ++c) s = __builtin_fmaf(qv[c], (float)kr[c], s);
-    mx = fmaxf(mx, s * cs);
-  }
+  for (int key = 0; key < a.tokens_kv; ++key) mx = fmaxf(mx, score(key) * cs);
   float l = 0.f;
-  for (int key = 0; key < a.tokens_kv; ++key) {
-    const bf16* kr = kb + (int64_t)key * a.k_sn;
-    const bf16* vr = vb + (int64_t)key * a.v_sn;
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < D; ++c) s = __builtin_fmaf(qv[c], (float)kr[c], s);
-    const float p = exp2f(__builtin_fmaf(s, cs, -mx));
-    l += p;
-#pragma unroll
-    for (int c = 0; c < D; ++c) acc[c] = __builtin_fmaf(p, (float)vr[c], acc[c]);
-  }
+  for (int key = 0; key < a.tokens_kv; ++key) l += exp2f(__builtin_fmaf(score(key), cs, -mx));
   const int FQ = a.frames * a.tokens_q;
   if (a.lse) a.lse[(int64_t)(b * a.heads + head) * FQ + qi] = mx + log2f(l);
   const float inv = 1.f / l;
   bf16* orow = static_cast<bf16*>(a.o) + b * a.o_sb + (int64_t)fr * a.o_sf + (int64_t)pos * a.o_sn + head * D;
+  for (int dc = 4 * h; dc < D; dc += 8) {        // this lane's 4-column slots of each 8-column group
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int key = 0; key < a.tokens_kv; ++key) {
+      const float p = exp2f(__builtin_fmaf(score(key), cs, -mx));
+      const bf16* vr = vb + (int64_t)key * a.v_sn + dc;
 #pragma unroll
-  for (int dc = 0; dc < D; dc += 8) {
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_fmaf(p, (float)vr[j], acc[j]);
+    }
     bf16x4 v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (bf16)((h ? acc[dc + 4 + j] : acc[dc + j]) * inv);
-    *reinterpret_cast<bf16x4*>(orow + dc + 4 * h) = v;
+    for (int j = 0; j < 4; ++j) v[j] = (bf16)(acc[j] * inv);
+    *reinterpret_cast<bf16x4*>(orow + dc) = v;
   }
 }
 
@@ -505,7 +328,7 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   using T = bf16;
   using M = Mfma<T>;
   using C = FrameCfg<T, D>;
-  static_assert(C::ONES && D <= 64 && D % 8 == 0, "x2f: bf16, spare ones row");
+  static_assert(C::ONES && D <= 80 && D % 8 == 0, "x2f: bf16, spare ones row");
   constexpr int NBLK = KT / 32;
   constexpr int NCH = (KT * C::CPR + 255) / 256;          // 16-byte chunks per thread per tile
   constexpr int LDS_BYTES = KT * (C::KROW + C::VROW) * 2;
@@ -694,39 +517,31 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   }
 }
 
-static int k1_variant() {  // VP2P_K1_VARIANT=0 / 2 / 4 / 5: one-set / x2 / x2f 128-key / x2f 256-key tiles (A/B)
-  const char* e = getenv("VP2P_K1_VARIANT");
-  return e ? atoi(e) : 5;
+static bool x2f_d80_off() {   // VP2P_K1_D80=1set: A/B switch for the res-32 layers, read once
+  static const bool off = [] {
+    const char* e = getenv("VP2P_K1_D80");
+    return e && e[0] == '1';
+  }();
+  return off;
 }
 
 template <typename T, int D>
 static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
   using C = FrameCfg<T, D>;
   const int FQ = a->frames * a->tokens_q;
-  if constexpr (C::BF && C::ONES && D <= 64) {
-    if (k1_variant() >= 4) {
-      const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
-      if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-      if (k1_variant() == 4) {
-        hipLaunchKernelGGL((frame_attn_kernel_x2f<D, 128>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);
-      } else {
-        constexpr int lds = 256 * (C::KROW + C::VROW) * 2;
-        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_x2f<D, 256>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
-        if (!attr) return VP2P_E_LAUNCH;
-        hipLaunchKernelGGL((frame_attn_kernel_x2f<D, 256>), dim3((unsigned)nwg), dim3(256), lds, stream, *a);
-      }
-      return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
-    }
+  if constexpr (C::BF && C::ONES && D <= 80) {
+    if (D > 64 && x2f_d80_off()) goto one_set;
+    constexpr int KT = D <= 64 ? 256 : 64;
+    constexpr int lds = KT * (C::KROW + C::VROW) * 2;
+    const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
+    if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_x2f<D, KT>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    if (!attr) return VP2P_E_LAUNCH;
+    hipLaunchKernelGGL((frame_attn_kernel_x2f<D, KT>), dim3((unsigned)nwg), dim3(256), lds, stream, *a);
+    return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
   }
-  if constexpr (C::BF && C::ONES && D <= 64) {
-    if (k1_variant() >= 2) {
-      const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
-      if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-      hipLaunchKernelGGL((frame_attn_kernel_x2<D>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);
-      return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
-    }
-  }
+one_set:
   const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 127) / 128);
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
   hipLaunchKernelGGL((frame_attn_kernel<T, D>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);
