@@ -1,0 +1,88 @@
+"""The frame-parallel VAE (vp2p.vae) vs the CPU restatement of diffusers 0.11.1
+AutoencoderKL (oracle/vae_ref.py; PARITY UNPINNED against the real library, which is not installed).
+
+Random-init SD-1.5 VAE config (no checkpoint offline).  fp32 within 1e-4 relative, bf16 within
+2e-2 relative to the reference's max |value| on a 64x64 image / 8x8 latent (every layer, the mid
+attention over 64 positions) and a 256x256 decode (attention over 1024 positions)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import vae_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def vae_state():
+    from vp2p.vae import AutoencoderKL, init_vae_random_
+    vae = init_vae_random_(AutoencoderKL(), seed=0)
+    return {k: v.clone() for k, v in vae.state_dict().items()}
+
+
+def _vae(state, dtype):
+    from vp2p.vae import AutoencoderKL
+    vae = AutoencoderKL()
+    vae.load_state_dict(state, strict=True)
+    return vae.to("cuda", dtype).to(memory_format=torch.channels_last).eval()
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max())
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("hw", [64, 256])
+def test_decode_matches_oracle(vae_state, dtype, tol, hw):
+    vae = _vae(vae_state, dtype)
+    g = torch.Generator().manual_seed(1)
+    z = torch.randn(2, 4, hw // 8, hw // 8, generator=g)
+    with torch.no_grad():
+        got = vae.decode(z.cuda()).float().cpu()
+    ref = vae_ref.decode(vae_state, z)
+    assert got.shape == ref.shape == (2, 3, hw, hw)
+    assert _rel(got, ref) < tol, _rel(got, ref)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+def test_encode_matches_oracle(vae_state, dtype, tol):
+    vae = _vae(vae_state, dtype)
+    g = torch.Generator().manual_seed(2)
+    img = torch.rand(3, 3, 64, 64, generator=g) * 2 - 1
+    with torch.no_grad():
+        got = vae.encode_mean(img.cuda()).float().cpu()
+    ref = vae_ref.encode_mean(vae_state, img)
+    assert got.shape == ref.shape == (3, 4, 8, 8)
+    assert _rel(got, ref) < tol, _rel(got, ref)
+
+
+def test_pipeline_helpers(vae_state):
+    """decode_latents (pipeline_tuneavideo.py:239-256: 1/0.18215, batches of 4 '(b f)' frames, clamp to
+    [0, 1], a trailing partial batch dropped as the reference loop does), image2latent_video /
+    latent2image_video (run_videop2p.py:505-537)."""
+    from vp2p import vae as V
+    vae = _vae(vae_state, torch.float32)
+    g = torch.Generator().manual_seed(3)
+    lat = torch.randn(2, 4, 4, 8, 8, generator=g)
+    with torch.no_grad():
+        video = V.decode_latents(vae, lat.cuda()).cpu()
+    ref = vae_ref.decode(vae_state, (lat / V.SCALING).permute(0, 2, 1, 3, 4).reshape(8, 4, 8, 8))
+    ref = (ref / 2 + 0.5).clamp(0, 1).reshape(2, 4, 3, 64, 64).permute(0, 2, 1, 3, 4)
+    assert video.shape == (2, 3, 4, 64, 64) and _rel(video, ref) < 1e-4
+    # 6 frames of one clip: the reference decodes range(max(6 // 4, 1)) = 1 batch -> 4 frames
+    with torch.no_grad():
+        short = V.decode_latents(vae, torch.randn(1, 4, 6, 8, 8, generator=g).cuda())
+    assert short.shape == (1, 3, 4, 64, 64)
+    frames = torch.randint(0, 256, (3, 64, 64, 3), generator=g, dtype=torch.uint8)
+    with torch.no_grad():
+        z = V.encode_video(vae, frames.cuda()).cpu()
+    img = frames.float() / 127.5 - 1
+    zref = vae_ref.encode_mean(vae_state, img.permute(0, 3, 1, 2)) * V.SCALING
+    assert z.shape == (1, 4, 3, 8, 8)
+    assert _rel(z[0].permute(1, 0, 2, 3), zref) < 1e-4
+    with torch.no_grad():
+        back = V.latent2image_video(vae, z.cuda()).cpu()
+    assert back.shape == (3, 64, 64, 3) and back.dtype == torch.uint8
+    img_ref = (vae_ref.decode(vae_state, z[0].permute(1, 0, 2, 3) / V.SCALING) / 2 + 0.5).clamp(0, 1)
+    img_ref = (img_ref.permute(0, 2, 3, 1) * 255).to(torch.uint8)
+    assert int((back.int() - img_ref.int()).abs().max()) <= 1

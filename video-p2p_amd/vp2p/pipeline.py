@@ -4,8 +4,8 @@
 CFG batch [uncond x P, cond x P], optional per-step null-text embeddings (``uncond_embeddings_pre``
 overwrites row 0, :399-403), fast mode (source row unguided, :412-415), DDIM step and the
 controller's step callback (LocalBlend).  With a vp2p controller the CFG + DDIM + LocalBlend tail
-of every step is ONE kernel (``ops.step_fused``).  VAE decoding is out of scope: the pipeline
-returns latents (``output_type="latent"``).
+of every step is ONE kernel (``ops.step_fused``).  ``output_type="tensor"`` decodes the edited
+latents with the pipeline's VAE (``vp2p.vae``, per frame, on the GPU); the default returns latents.
 
 ``NullInversion.ddim_loop`` / ``invert_`` / ``invert`` follow run_videop2p.py:557-567 / :626-635 /
 :614-624 on latents (image loading and the VAE encoder are out of scope).  ``null_optimization``
@@ -27,11 +27,13 @@ GUIDANCE_SCALE = 7.5
 
 
 class VideoP2PPipeline:
-    def __init__(self, unet, scheduler: Optional[DDIMScheduler] = None, tokenizer=None, text_encoder=None):
+    def __init__(self, unet, scheduler: Optional[DDIMScheduler] = None, tokenizer=None, text_encoder=None,
+                 vae=None):
         self.unet = unet
         self.scheduler = scheduler or DDIMScheduler()
         self.tokenizer = tokenizer
         self.text_encoder = text_encoder
+        self.vae = vae
 
     @property
     def device(self):
@@ -62,8 +64,10 @@ class VideoP2PPipeline:
         LocalBlend), as in pipeline_tuneavideo.py:427-430."""
         if eta != 0.0:
             raise NotImplementedError("eta > 0 is out of scope (deterministic DDIM only)")
-        if output_type != "latent":
-            raise NotImplementedError("VAE decoding is out of scope; use output_type='latent'")
+        if output_type not in ("latent", "tensor"):
+            raise ValueError("output_type: 'latent' (the edited latents) or 'tensor' (decoded video in [0, 1])")
+        if output_type == "tensor" and self.vae is None:
+            raise ValueError("output_type='tensor' needs the pipeline's vae (vp2p.vae.AutoencoderKL)")
         prompts = [prompt] if isinstance(prompt, str) else list(prompt)
         P = len(prompts)
         dev = self.device
@@ -112,6 +116,9 @@ class VideoP2PPipeline:
                 lat = controller.step_callback(lat).to(dev, torch.float32)
             if callback is not None and i % callback_steps == 0:
                 callback(i, t, lat)
+        if output_type == "tensor":             # decode_latents (pipeline_tuneavideo.py:433-437)
+            from .vae import decode_latents
+            return decode_latents(self.vae, lat)
         return lat
 
 
