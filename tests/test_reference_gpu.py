@@ -98,7 +98,7 @@ def sd15_state():
     return model_state(UNet3DConditionModel, 44)
 
 
-# whole UNet (60+ layers): fp32 within 1e-4 of the reference's max; bf16 PSNR >= 40 dB
+# whole UNet (60+ layers): fp32 within 1e-4 of the reference's max; bf16 PSNR >= 44 dB (measured 47-48)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_unet_sd15_vs_reference(golden_models, sd15_state, dtype):
     """The SD-1.5-geometry UNet3D (d = 40 / 80 / 160, 16 transformer blocks, 22 resnets) on a
@@ -114,7 +114,7 @@ def test_unet_sd15_vs_reference(golden_models, sd15_state, dtype):
     if dtype == torch.float32:
         assert _rel(got, ref) < 1e-4, _rel(got, ref)
     else:
-        assert psnr(got, ref) >= 40.0, psnr(got, ref)
+        assert psnr(got, ref) >= 44.0, psnr(got, ref)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -141,7 +141,7 @@ def test_unet_controlled_vs_reference(golden_models, sd15_state, tokenizer, dtyp
     if dtype == torch.float32:
         assert _rel(got, ref) < 1e-4, _rel(got, ref)
     else:
-        assert psnr(got, ref) >= 40.0, psnr(got, ref)
+        assert psnr(got, ref) >= 44.0, psnr(got, ref)
 
 
 # -- end-to-end edits ---------------------------------------------------------------------------------
@@ -202,9 +202,10 @@ def _edit_fixture(name):
     return np.load(path)
 
 
-# End-to-end bars: fp32 -- final-latent PSNR >= 60 dB and LocalBlend masks equal to
-# the reference's up to pixels whose map value sits within 1e-3 of the threshold; bf16 -- PSNR >= 30 dB.
-@pytest.mark.parametrize("dtype,bar", [(torch.float32, 60.0), (torch.bfloat16, 30.0)])
+# End-to-end bars: fp32 -- final-latent PSNR >= 100 dB and LocalBlend masks equal to the
+# reference's (at most 1 flip per 10^4 pixels); bf16 -- final-latent PSNR >= 45 dB.
+# Measured (profiles/r02_parity_reference.jsonl): fp32 119-121 dB, bf16 50.7-51.3 dB, 0 mask flips.
+@pytest.mark.parametrize("dtype,bar", [(torch.float32, 100.0), (torch.bfloat16, 45.0)])
 @pytest.mark.parametrize("name", ["car2", "rabbit8", "penguin24"])
 def test_edit_vs_reference_pipeline(tokenizer, bench_state, name, dtype, bar):
     gold = _edit_fixture(name)

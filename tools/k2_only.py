@@ -1,5 +1,6 @@
 """Runs K2 (cross-attention + fused P2P refine/reweight edit, cond + uncond halves) at one edit
-shape N times, for PMC passes: python tools/k2_only.py [N] [hw] [C]."""
+shape N times, for PMC passes: python tools/k2_only.py [N] [hw] [C] [step]
+(step < 10: an edit launch; step >= 10: the plain/LocalBlend-free launch of the later steps)."""
 import os
 import sys
 
@@ -17,6 +18,7 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     hw = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     C = int(sys.argv[3]) if len(sys.argv) > 3 else 320
+    step = int(sys.argv[4]) if len(sys.argv) > 4 else 3
     prompts, swap, blend, eq, cross, self_ = __import__("bench").RABBIT
     ctrl = vp2p.make_controller(prompts, swap, {"default_": cross}, self_, blend, eq,
                                 tokenizer=SyntheticCLIPTokenizer(), num_steps=50)
@@ -27,7 +29,7 @@ def main():
     k = torch.randn(B, 77, C, device="cuda", dtype=torch.bfloat16, generator=g)
     v = torch.randn(B, 77, C, device="cuda", dtype=torch.bfloat16, generator=g)
     for _ in range(n):
-        ops.cross_attention_p2p(q, k, v, f, heads, plan=plan, step=3)
+        ops.cross_attention_p2p(q, k, v, f, heads, plan=plan, step=step, edit=step < 10)
     torch.cuda.synchronize()
 
 

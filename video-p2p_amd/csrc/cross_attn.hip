@@ -329,20 +329,19 @@ void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// K2 v2 (bf16, d <= 64, two prompts): K/V live in REGISTERS, waves are persistent.
+// K2 v2 (bf16, d <= 64): the launches WITHOUT an edit (every uncond half, and the cond half outside
+// the cross-replace window: 40 of the 50 steps), with K/V in REGISTERS and persistent waves.
 //
 // The 77-key K/V of one (batch row, head) is the same for every query block, so each wave loads its
 // row's K fragments (KB x KS) and V^T fragments (NT x KB x 2) once and then streams query blocks:
 // per block only Q (prefetched one block ahead) comes in and O goes out -- the HBM traffic the
 // roofline counts -- with no K/V re-reads through L2 per block (the v1 kernel's 21 KB per wave and
-// prompt) and no per-block dependency on a K/V fetch.
-// Waves pair up on the prompts of one CFG half: wave 2s+p runs prompt p of query stream s.  In the
-// conditional half the source wave (p = 0) parks its probabilities in an LDS ring (two slots per
-// pair) and the edited wave (p = 1) reads them after one workgroup barrier per block (run_videop2p.py
-// :304-317); the unconditional half / plain batches need no exchange.
+// prompt) and no per-block dependency on a K/V fetch.  Wave w runs prompt (w & 1) of query stream
+// (w >> 1) of a CFG half (two prompts), or stream w of a plain batch row.  Softmax normalisation
+// moves to O (flash-style) unless something reads the probabilities (LocalBlend sum, stored maps).
 // ------------------------------------------------------------------------------------------------
 template <int D, int KB>
-__global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_attn_args a, int prow, int iters) {
+__global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_attn_args a, int iters) {
   using T = bf16;
   using M = Mfma<T>;
   using C = CrossCfg<T, D>;
@@ -355,34 +354,20 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
   const int g = blockIdx.y;                    // CFG half (p2p) or batch row
   const int head = blockIdx.z;
   const bool cond = p2p && (a.cond_only || g == 1);
-  const bool edit = cond && (a.edit_mode != VP2P_EDIT_NONE || a.reweight);
   const bool lb = cond && a.lb_acc != nullptr;
   const int NKV = a.tokens_kv;
-  // wave roles: p2p -> (prompt, stream) = (w & 1, w >> 1), 2 streams; plain -> prompt 0, 4 streams
   const int pw = p2p ? (w & 1) : 0;
   const int sw = p2p ? (w >> 1) : w;
   const int NS = p2p ? 2 : 4;
   const int b = p2p ? g * 2 + pw : g;          // batch row of this wave
 
-  float* ring = reinterpret_cast<float*>(smem);                      // [2 streams][2 slots][32][prow]
-  f32x4* etab = reinterpret_cast<f32x4*>(ring + 2 * 2 * 32 * prow);  // [NKV] (one edited prompt)
-  float* lbw = reinterpret_cast<float*>(etab + NKV);                  // [sets][2][NKV]
+  float* lbw = reinterpret_cast<float*>(smem);  // [sets][2][NKV]
   const int LBS = a.lb_sets == 2 ? 2 : 1;
-  if (edit) {
-    for (int i = tid; i < NKV; i += 256) {
-      f32x4 t;
-      t[0] = a.edit_mode == VP2P_EDIT_REFINE ? a.refine_alpha[i] : 0.f;
-      t[1] = a.reweight ? a.equalizer[i] : 1.f;
-      t[2] = a.alpha_words[i];
-      t[3] = __int_as_float(a.edit_mode == VP2P_EDIT_REFINE ? a.map_idx[i] : i);
-      etab[i] = t;
-    }
-  }
-  if (lb)
+  if (lb) {
     for (int i = tid; i < LBS * 2 * NKV; i += 256) lbw[i] = a.lb_word_alpha[i];
-  __syncthreads();
+    __syncthreads();
+  }
 
-  // this wave's K (A fragments of S^T) and V^T (A fragments of O^T), resident for the whole loop
   const T* ws = static_cast<const T*>(a.kv_ws);
   const int64_t kelems = (int64_t)a.batch * a.heads * KP * C::DP;
   const T* kb_base = ws + ((int64_t)(b * a.heads + head) * KP) * C::DP;
@@ -401,29 +386,41 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
   }
 
   const float cs = a.scale * kLog2e;
-  const int qb0 = blockIdx.x * NS * iters + sw;    // this stream's blocks: qb0, qb0 + NS, ...
-  auto load_q = [&](int qb, bf16x8* dst) {
-    const int qi = qb * 32 + r;
-    const bool ok = qb < qblocks && qi < FQ;
-    const int fr = ok ? qi / a.tokens_q : 0;
-    const int pos = ok ? qi - fr * a.tokens_q : 0;
-    const T* row = static_cast<const T*>(a.q) + b * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * D;
+  const bool norm_p = lb || a.probs_out;
+  // this stream's query blocks: qb0, qb0 + NS, ...; (frame, token) of the lane's query tracked
+  // incrementally (no integer division in the loop)
+  const int qb0 = blockIdx.x * NS * iters + sw;
+  const int step = 32 * NS;
+  const T* qbase = static_cast<const T*>(a.q) + b * a.q_sb + head * D;
+  T* obase = static_cast<T*>(a.o) + b * a.o_sb + head * D;
+  int qi = qb0 * 32 + r;
+  int fr = qi / a.tokens_q, pos = qi - (qi / a.tokens_q) * a.tokens_q;
+  auto advance = [&](int& f_, int& p_) {
+    p_ += step;
+    while (p_ >= a.tokens_q) { p_ -= a.tokens_q; ++f_; }
+  };
+  auto load_q = [&](int qi_, int f_, int p_, bf16x8* dst) {
+    const bool ok = qi_ < FQ;
+    const T* row = qbase + (ok ? f_ * a.q_sf + p_ * a.q_sn : 0);
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) dst[s] = ok ? M::row_frag(row, s, h, D) : M::zero();
   };
   bf16x8 qn[C::KS];
-  load_q(qb0, qn);
+  load_q(qi, fr, pos, qn);
+  int fr_n = fr, pos_n = pos;
 
   for (int it = 0; it < iters; ++it) {
-    const int qb = qb0 + it * NS;
     bf16x8 qf[C::KS];
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) qf[s] = qn[s];
-    if (it + 1 < iters) load_q(qb + NS, qn);
-    const int qi = qb * 32 + r;
-    const bool qv = qb < qblocks && qi < FQ;
-    const int fr = qv ? qi / a.tokens_q : 0;
-    const int pos = qv ? qi - fr * a.tokens_q : 0;
+    const int qcur = qi;
+    const int fcur = fr_n, pcur = pos_n;
+    if (it + 1 < iters) {        // next block's Q (prefetching two ahead measured slower: 60 vs 56 us)
+      advance(fr_n, pos_n);
+      qi += step;
+      load_q(qi, fr_n, pos_n, qn);
+    }
+    const bool qv = qcur < FQ;
 
     f32x16 sc[KB];
 #pragma unroll
@@ -432,8 +429,7 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
 #pragma unroll
       for (int s = 0; s < C::KS; ++s) sc[kb] = M::mma(kf[kb][s], qf[s], sc[kb]);
     }
-    // row softmax: only the last key block is ragged (keys >= NKV masked); max on raw scores,
-    // exp2(s * cs - max * cs) as one fma
+    // row softmax: only the last key block is ragged; max on raw scores, exp2(s*cs - max*cs) fused
     float mx = kNegInf;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
@@ -454,80 +450,38 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
       }
     sum += xhalf(sum);
     const float inv = 1.f / sum;
-    // probabilities are read (edit, LocalBlend sum, stored maps): normalise them; otherwise 1/sum is
-    // applied to O at the end (flash-style; the same softmax, fewer VALU ops per score)
-    const bool norm_p = edit || lb || a.probs_out;
     if (norm_p) {
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) sc[kb][i] *= inv;
+      if (lb) {  // this head's word-weighted map of token qi -> lb_ws[set][p][head][qi]
+        for (int set = 0; set < LBS; ++set) {
+          const float* wts = lbw + (set * 2 + pw) * NKV;
+          float part = 0.f;
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int wd = kb * 32 + acc_row(i, h);
+              if (wd < NKV) part += wts[wd] * sc[kb][i];
+            }
+          part += xhalf(part);
+          if (h == 0 && qv) a.lb_ws[((int64_t)(set * 2 + pw) * a.heads + head) * FQ + qcur] = part;
+        }
+      }
+      if (a.probs_out && qv) {
+        float* prow_out = a.probs_out + ((((int64_t)b * a.frames + fcur) * a.heads + head) * a.tokens_q + pcur) * NKV;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) prow_out[wd] = sc[kb][i];
+          }
+      }
     }
     const float oscale = norm_p ? 1.f : inv;
-
-    if (edit) {
-      float* slot = ring + ((sw * 2 + (it & 1)) * 32 + r) * prow;
-      if (pw == 0) {
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int wd = kb * 32 + acc_row(i, h);
-            if (wd < NKV) slot[wd] = sc[kb][i];
-          }
-      }
-      __syncthreads();                         // source probabilities of this block are parked
-      if (pw == 1) {
-#pragma clang fp contract(off)
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int wd = kb * 32 + acc_row(i, h);
-            if (wd < NKV) {
-              const float pe_val = sc[kb][i];
-              const f32x4 t = etab[wd];
-              float R;
-              if (a.edit_mode == VP2P_EDIT_REPLACE) {
-                float gsum = 0.f;
-                for (int n = a.map_ptr[wd]; n < a.map_ptr[wd + 1]; ++n) gsum += slot[a.map_idx[n]] * a.map_val[n];
-                R = gsum;
-              } else if (a.edit_mode == VP2P_EDIT_REFINE) {
-                R = slot[__float_as_int(t[3])] * t[0] + pe_val * (1.f - t[0]);
-              } else {
-                R = slot[wd];
-              }
-              R = R * t[1];
-              sc[kb][i] = R * t[2] + (1.f - t[2]) * pe_val;
-            }
-          }
-      }
-    }
-    if (lb) {  // this head's word-weighted map of token qi -> lb_ws[set][p][head][qi]
-      for (int set = 0; set < LBS; ++set) {
-        const float* wts = lbw + (set * 2 + pw) * NKV;
-        float part = 0.f;
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int wd = kb * 32 + acc_row(i, h);
-            if (wd < NKV) part += wts[wd] * sc[kb][i];
-          }
-        part += xhalf(part);
-        if (h == 0 && qv) a.lb_ws[((int64_t)(set * 2 + pw) * a.heads + head) * FQ + qi] = part;
-      }
-    }
-    if (a.probs_out && qv) {
-      float* prow_out = a.probs_out + ((((int64_t)b * a.frames + fr) * a.heads + head) * a.tokens_q + pos) * NKV;
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int wd = kb * 32 + acc_row(i, h);
-          if (wd < NKV) prow_out[wd] = sc[kb][i];
-        }
-    }
     f32x16 o[C::NT];
 #pragma unroll
     for (int t = 0; t < C::NT; ++t) o[t] = zero16();
@@ -540,7 +494,7 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
         for (int t = 0; t < C::NT; ++t) o[t] = M::mma(vf[kb][sp][t], pf, o[t]);
       }
     if (qv) {
-      T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr * a.o_sf + pos * a.o_sn + head * D;
+      T* orow = obase + fcur * a.o_sf + pcur * a.o_sn;
 #pragma unroll
       for (int t = 0; t < C::NT; ++t)
 #pragma unroll
@@ -617,12 +571,10 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
       const int iters = (int)((per_group + nx - 1) / nx);
       nx = (per_group + iters - 1) / iters;
       if (gh > 65535 * 64 || nx > 0x7fffffff) return VP2P_E_SHAPE;
-      const int prow = a->tokens_kv | 1;
       const int sets = a->lb_sets == 2 ? 2 : 1;
-      const size_t lds = (size_t)2 * 2 * 32 * prow * sizeof(float) + (size_t)a->tokens_kv * 16 +
-                         (size_t)sets * 2 * a->tokens_kv * sizeof(float);
+      const size_t lds = (size_t)sets * 2 * a->tokens_kv * sizeof(float);
       hipLaunchKernelGGL((cross_attn_kernel_v2<D, KB>), dim3((unsigned)nx, (unsigned)groups, (unsigned)a->heads),
-                         dim3(256), lds, s, *a, prow, iters);
+                         dim3(256), lds, s, *a, iters);
       if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
       if (p2p && a->lb_acc) {
         const int64_t n = (int64_t)sets * a->prompts * FQ;
