@@ -1,6 +1,7 @@
 """HBM bytes per launch of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
 
-usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV KERNEL_SUBSTR OUT_JSON [ALG_BYTES]
+usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV KERNEL_SUBSTR OUT_JSON [ALG_BYTES] [SHAPE]
+SHAPE: the launch's q shape, e.g. 32,4096,320 (bench.py uses the file only for that shape).
 
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE on gfx950 counts half the bytes of a wide
 coalesced streaming read -> doubled here; WRITE_SIZE is exact for 16-B/lane stores.  Both are in KB.
@@ -23,6 +24,7 @@ def per_dispatch(path, counter, sub):
 def main():
     fetch_csv, write_csv, sub, out = sys.argv[1:5]
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    shape = [int(x) for x in sys.argv[6].split(",")] if len(sys.argv) > 6 else None
     fe = per_dispatch(fetch_csv, "FETCH_SIZE", sub)
     wr = per_dispatch(write_csv, "WRITE_SIZE", sub)
     if not fe or not wr:
@@ -32,6 +34,8 @@ def main():
     res = {"kernel_substr": sub, "dispatches": [len(fe), len(wr)], "fetch_bytes": fetch, "write_bytes": write,
            "bytes_per_launch": round(fetch + write),
            "how": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE in separate passes"}
+    if shape:
+        res["shape"] = shape
     if alg:
         res["algorithmic_bytes"] = alg
         res["traffic_over_algorithmic"] = round((fetch + write) / alg, 3)
