@@ -77,12 +77,14 @@ def test_frame_attention_large_logits():
     assert _rel(_np(out), ref) < 1e-4
 
 
-@pytest.mark.parametrize("spike", [4.0, 12.0, "overflow"])
+@pytest.mark.parametrize("spike", [4.0, 12.0, "overflow", "overflow_v"])
 def test_frame_attention_bf16_spikes(spike):
     """bf16 d=40 (the x2f kernel): a late key whose logits jump far above the first block's max.
     4x / 12x exercise the row-sum rescale; "overflow" aligns the key with one query so that its logit
     is ~100 nats above the running max (p would overflow bf16/fp32), forcing the exact per-row
-    fallback.  Tolerance: the bf16 bar of the north star, 2e-2 of max|ref|."""
+    fallback; "overflow_v" puts the logit ~80 nats up (p ~ 2^114, the row sum stays finite) on a
+    value row of magnitude 2^20, so only the O accumulator overflows -- the fallback must catch that
+    too.  Tolerance: the bf16 bar of the north star, 2e-2 of max|ref|."""
     from vp2p import ops
     heads, B, frames, n, d = 8, 1, 2, 512, 40
     C = heads * d
@@ -91,9 +93,14 @@ def test_frame_attention_bf16_spikes(spike):
     if spike == "overflow":
         k[0, 450, :d] = 16.0 * q[1, 100, :d]
         k[0, 300, d:2 * d] = 12.0 * q[0, 7, d:2 * d]
+    elif spike == "overflow_v":      # logit of query (1, 100) on key 450: 80 nats (p ~ 2^115)
+        qq = float((q[1, 100, :d].double() ** 2).sum())
+        k[0, 450, :d] = (80.0 * d ** 0.5 / qq) * q[1, 100, :d]
     else:
         k[0, 450] *= spike
     v = _rand((B * frames, n, C), 6, 1.0)
+    if spike == "overflow_v":
+        v[0, 450, :d] *= 2.0 ** 20
     q, k, v = (x.to(torch.bfloat16) for x in (q, k, v))
     ref = O.frame_attention(_np(q), _np(k), _np(v), frames, heads)
     assert np.isfinite(ref).all()

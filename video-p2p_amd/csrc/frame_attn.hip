@@ -494,8 +494,14 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
     const float mine = o[st][C::ONE_T][C::ONE_I];
     const float other = xhalf(mine);
     const float lrow = (h == C::ONE_H) ? mine : other;
-    // inf / NaN by exponent bits (the file builds with -fno-honor-nans)
-    const bool bad = qv[st] && (__float_as_uint(lrow) & 0x7f800000u) == 0x7f800000u;
+    // inf / NaN by exponent bits (the file builds with -fno-honor-nans), in the row sum or in any of
+    // this lane's O values (p <= 2^127 between growth checks times |v| > 2 can overflow O while l
+    // stays finite)
+    bool bad = qv[st] && (__float_as_uint(lrow) & 0x7f800000u) == 0x7f800000u;
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bad |= qv[st] && (__float_as_uint(o[st][t][i]) & 0x7f800000u) == 0x7f800000u;
     if (qv[st] && !bad) {
       if (a.lse) a.lse[(int64_t)(b * a.heads + head) * FQ + qi[st]] = m[st] + log2f(lrow);
       const float inv = 1.f / lrow;
