@@ -182,7 +182,7 @@ class AttnTimer:
             roof = {"bound": "mfma", "achieved": k1["tflops"], "peak": peak, "unit": "TFLOP/s",
                     "frac": round(k1["tflops"] / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                     "traffic_source": src, "algorithmic_bytes": k1["bytes_per_launch"],
-                    "kernel": "vp2p::frame_attn_kernel_x2f<40,256> (res-64 FrameAttention)",
+                    "kernel": "vp2p::frame_attn_kernel_x2f<40,128,true> (res-64 FrameAttention, folded max)",
                     "launches": sum(1 for ev in self.events["frame_attention"] if ev[2][1] == k1["tokens"]),
                     "avg_ms": k1["avg_ms"], "flops_per_launch": k1["flop_per_launch"], "shape": k1["shape"]}
         attn = {"mfma_util": round(tot_flop / (tot_ms / 1e3) / 1e12 / peak, 4),
@@ -276,7 +276,8 @@ def k1long_main(args, world, rank, dev):
     g = torch.Generator(device=dev).manual_seed(3 + rank)
     bufs = []
     for hw, C, n in levels:
-        q = torch.randn(B * fl, hw, C, device=dev, dtype=torch.bfloat16, generator=g)
+        # q as the to_q GEMM hands it to K1 (scale * log2 e folded in: FrameAttention.forward)
+        q = (torch.randn(B * fl, hw, C, device=dev, generator=g) * ops.frame_query_scale(C // heads)).bfloat16()
         x0 = torch.randn(B, hw, C, device=dev, dtype=torch.bfloat16, generator=g)
         wkv = torch.randn(2 * C, C, device=dev, dtype=torch.bfloat16, generator=g) * C ** -0.5
         bufs.append((q, x0, wkv, torch.empty_like(q), C, n))
@@ -287,7 +288,7 @@ def k1long_main(args, world, rank, dev):
                 if world > 1:
                     dist.broadcast(x0, src=0)
                 kv = F.linear(x0, wkv)
-                ops.frame_attention(q, kv[..., :C], kv[..., C:], fl, heads, out=out)
+                ops.frame_attention(q, kv[..., :C], kv[..., C:], fl, heads, out=out, q_prescaled=True)
 
     for _ in range(args.warmup):
         step()

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 7
+#define VP2P_ABI_VERSION 8
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -66,6 +66,10 @@ typedef struct vp2p_frame_attn_args {
   int32_t dtype;            /* vp2p_dtype of q/k/v/o */
   float* lse;               /* optional (batch, heads, frames*tokens_q) fp32: log2 of each query row's
                              * sum_k exp2(score*scale*log2(e)), for the backward; NULL = off */
+  int32_t q_prescaled;      /* 1: q already holds q * scale * log2(e) (the caller folded the softmax
+                             * scale into its projection, e.g. as the GEMM's alpha: one rounding);
+                             * `scale` is then ignored and lse is in the same units.  Selects the
+                             * folded-max kernel at head_dim 40 (bf16). */
 } vp2p_frame_attn_args;
 
 int vp2p_frame_attn_fwd(const vp2p_frame_attn_args* args, void* stream);

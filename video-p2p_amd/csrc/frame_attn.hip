@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
     }
   };
 
-  const float cs = a.scale * kLog2e;
+  const float cs = a.q_prescaled ? 1.f : a.scale * kLog2e;
   float m = kNegInf;            // running max of s*cs (log2 units), shared by lanes r and r+32
   float lsum = 0.f;             // only without the ones row
   f32x16 o[C::NT];
@@ -323,12 +323,26 @@ __device__ __forceinline__ void frame_attn_exact_row(const vp2p_frame_attn_args&
   }
 }
 
-template <int D, int KT>
+// Two forms of the inner loop:
+//   FOLD = false: p = exp2(s * c - m) (c = scale * log2 e): one v_fma + one v_exp + half a v_cvt per
+//                 score; set 0's QK^T then set 1's, then the two softmax + PV halves;
+//   FOLD = true (the caller passed q already multiplied by c -- its projection GEMM's alpha -- and the
+//                 head dim has a padding column in the QK^T k-steps, d = 40: 48): -m rides in the MFMA
+//                 through that column (Q'[D] = -m held exactly in bf16, K[D] = 1 in the LDS image), so
+//                 the accumulator already holds s * c - m and the softmax is one v_exp + half a v_cvt
+//                 per score.  m is kept bf16-representable and O is rescaled by the exact
+//                 exp2(m_old - m_new) when it moves.  The blocks are set-staggered: set 1's QK^T of
+//                 block j and set 0's QK^T of block j + 1 are issued ahead of the other set's softmax,
+//                 so each set's exp/cvt run under MFMAs (128-key tiles keep the extra score registers
+//                 within the 2-waves/SIMD budget).
+template <int D, int KT, bool FOLD>
 __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame_attn_args a) {
   using T = bf16;
   using M = Mfma<T>;
   using C = FrameCfg<T, D>;
   static_assert(C::ONES && D <= 80 && D % 8 == 0, "x2f: bf16, spare ones row");
+  static_assert(!FOLD || C::DP > D, "folded max needs a padding column in the QK^T k-steps");
+  constexpr int PAD_S = D / 16, PAD_H = (D % 16) / 8, PAD_J = D % 8;   // qf slot of column D
   constexpr int NBLK = KT / 32;
   constexpr int NCH = (KT * C::CPR + 255) / 256;          // 16-byte chunks per thread per tile
   constexpr int LDS_BYTES = KT * (C::KROW + C::VROW) * 2;
@@ -342,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   const int bh = bid / qblocks, qb = bid - bh * qblocks;
   const int b = bh / a.heads, head = bh - b * a.heads;
   const int Nk = a.tokens_kv;
-  const float cs = a.scale * kLog2e;
+  const float cs = a.q_prescaled ? 1.f : a.scale * kLog2e;
 
   int qi[2], fr[2], pos[2];
   bool qv[2];
@@ -359,7 +373,10 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   }
   for (int i = tid; i < LDS_BYTES / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0, 0, 0, 0};
   __syncthreads();
-  for (int k = tid; k < KT; k += 256) Vs[k * C::VROW + D] = (T)1.0f;   // O^T row D = sum_k p
+  for (int k = tid; k < KT; k += 256) {
+    Vs[k * C::VROW + D] = (T)1.0f;                 // O^T row D = sum_k p
+    if constexpr (FOLD) Ks[k * C::KROW + D] = (T)1.0f;   // S^T += 1 * Q'[D] = -m
+  }
 
   const T* kbase = static_cast<const T*>(a.k) + b * a.k_sb + head * D;
   const T* vbase = static_cast<const T*>(a.v) + b * a.v_sb + head * D;
@@ -398,6 +415,14 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
 #pragma unroll
     for (int t = 0; t < C::NT; ++t) o[st][t] = zero16();
 
+  // folded max: the Q' slot of column D holds -m (lanes of half PAD_H own that column)
+  auto set_negm = [&](int st) {
+    if constexpr (FOLD) {
+      const bf16 nm = (bf16)(-m[st]);
+      if (h == PAD_H) qf[st][PAD_S][PAD_J] = nm;   // the other half holds column D - 8 (real data)
+    }
+  };
+
   // m starts at the exact row max of keys 0..31 (tile 0 in LDS; ragged Nk < 32 masked)
   auto init_max = [&]() {
 #pragma unroll
@@ -409,7 +434,12 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
       float v = kNegInf;
 #pragma unroll
       for (int i = 0; i < 16; ++i) v = fmaxf(v, acc_row(i, h) < Nk ? s[i] : kNegInf);
-      m[st] = fmaxf(v, xhalf(v)) * cs;
+      if constexpr (FOLD) {
+        m[st] = (float)(bf16)fmaxf(v, xhalf(v));   // already in log2 units; bf16-exact offset
+        set_negm(st);
+      } else {
+        m[st] = fmaxf(v, xhalf(v)) * cs;
+      }
     }
   };
 
@@ -428,25 +458,45 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
       return acc;
     };
     auto softmax_pv = [&](f32x16& sc, int key0, int st) {
-      const float nm = -m[st];
+      if constexpr (FOLD) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sc[i] = fast_exp2(__builtin_fmaf(sc[i], cs, nm));
+        for (int i = 0; i < 16; ++i) sc[i] = fast_exp2(sc[i]);
+      } else {
+        const float nm = -m[st];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[i] = fast_exp2(__builtin_fmaf(sc[i], cs, nm));
+      }
       const bf16x8 p0 = M::p_frag(sc, 0), p1 = M::p_frag(sc, 1);
 #pragma unroll
       for (int t = 0; t < C::NT; ++t) o[st][t] = M::mma(vt_frag_lds<C::VROW>(Vs, key0, 0, t), p0, o[st][t]);
 #pragma unroll
       for (int t = 0; t < C::NT; ++t) o[st][t] = M::mma(vt_frag_lds<C::VROW>(Vs, key0, 1, t), p1, o[st][t]);
     };
-    // set 0's QK^T, then set 1's, so set 0's softmax runs while set 1's MFMAs execute and set 1's
-    // softmax while set 0's PV MFMAs execute (the other wave of the SIMD fills the rest)
+    if constexpr (FOLD) {
+      // set-staggered: s0 of block j was issued during block j - 1
+      const int nblk = MASKED ? min(NBLK, (Nk - kt + 31) >> 5) : NBLK;
+      f32x16 s0 = qk(0, 0);
 #pragma unroll
-    for (int j = 0; j < NBLK; ++j) {
-      const int key0 = 32 * j;
-      if (MASKED && kt + key0 >= Nk) break;
-      f32x16 s0 = qk(key0, 0);
-      f32x16 s1 = qk(key0, 1);
-      softmax_pv(s0, key0, 0);
-      softmax_pv(s1, key0, 1);
+      for (int j = 0; j < NBLK; ++j) {
+        if (MASKED && j >= nblk) break;
+        const int key0 = 32 * j;
+        f32x16 s1 = qk(key0, 1);
+        softmax_pv(s0, key0, 0);
+        if (j + 1 < NBLK && (!MASKED || j + 1 < nblk)) s0 = qk(key0 + 32, 0);
+        softmax_pv(s1, key0, 1);
+      }
+    } else {
+      // set 0's QK^T, then set 1's, so set 0's softmax runs while set 1's MFMAs execute and set 1's
+      // softmax while set 0's PV MFMAs execute (the other wave of the SIMD fills the rest)
+#pragma unroll
+      for (int j = 0; j < NBLK; ++j) {
+        const int key0 = 32 * j;
+        if (MASKED && kt + key0 >= Nk) break;
+        f32x16 s0 = qk(key0, 0);
+        f32x16 s1 = qk(key0, 1);
+        softmax_pv(s0, key0, 0);
+        softmax_pv(s1, key0, 1);
+      }
     }
     // once per tile: the tile's row sum (valid on lanes h == ONE_H; the other half reads a zero row)
     float lc[2];
@@ -459,13 +509,21 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
         const float other = xhalf(mine);
         const float dl = h == C::ONE_H ? mine : other;
         const float delta = dl > kSumThr ? __log2f(dl) : 0.f;   // rows that did not grow: alpha = 1
-        const float alpha = fast_exp2(-delta);
+        float alpha;
+        if constexpr (FOLD) {
+          const float mn = dl > kSumThr ? (float)(bf16)(m[st] + delta) : m[st];
+          alpha = fast_exp2(m[st] - mn);
+          m[st] = mn;
+          set_negm(st);
+        } else {
+          alpha = fast_exp2(-delta);
+          m[st] += delta;
+        }
 #pragma unroll
         for (int t = 0; t < C::NT; ++t)
 #pragma unroll
           for (int i = 0; i < 16; ++i) o[st][t][i] *= alpha;
         lc[st] *= alpha;
-        m[st] += delta;
       }
     }
     lp[0] = lc[0];
@@ -531,6 +589,16 @@ static bool x2f_d80_off() {   // VP2P_K1_D80=1set: A/B switch for the res-32 lay
   return off;
 }
 
+template <int D, int KT, bool FOLD>
+static int launch_x2f(const vp2p_frame_attn_args* a, int64_t nwg, hipStream_t stream) {
+  constexpr int lds = KT * (FrameCfg<bf16, D>::KROW + FrameCfg<bf16, D>::VROW) * 2;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_x2f<D, KT, FOLD>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  if (!attr) return VP2P_E_LAUNCH;
+  hipLaunchKernelGGL((frame_attn_kernel_x2f<D, KT, FOLD>), dim3((unsigned)nwg), dim3(256), lds, stream, *a);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
 template <typename T, int D>
 static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
   using C = FrameCfg<T, D>;
@@ -538,14 +606,11 @@ static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
   if constexpr (C::BF && C::ONES && D <= 80) {
     if (D > 64 && x2f_d80_off()) goto one_set;
     constexpr int KT = D <= 64 ? 256 : 64;
-    constexpr int lds = KT * (C::KROW + C::VROW) * 2;
     const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
     if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_x2f<D, KT>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
-    if (!attr) return VP2P_E_LAUNCH;
-    hipLaunchKernelGGL((frame_attn_kernel_x2f<D, KT>), dim3((unsigned)nwg), dim3(256), lds, stream, *a);
-    return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+    if constexpr (C::DP > D)
+      if (a->q_prescaled) return launch_x2f<D, 128, true>(a, nwg, stream);
+    return launch_x2f<D, KT, false>(a, nwg, stream);
   }
 one_set:
   const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 127) / 128);

@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
@@ -60,7 +60,7 @@ class FrameAttnArgs(ctypes.Structure):
                 ("o_sb", c_int64), ("o_sf", c_int64), ("o_sn", c_int64),
                 ("batch", c_int32), ("frames", c_int32), ("tokens_q", c_int32), ("tokens_kv", c_int32),
                 ("heads", c_int32), ("head_dim", c_int32), ("scale", c_float), ("dtype", c_int32),
-                ("lse", c_void_p)]
+                ("lse", c_void_p), ("q_prescaled", c_int32)]
 
 
 class FrameAttnBwdArgs(ctypes.Structure):

@@ -38,6 +38,16 @@ def _cat_weight(module: nn.Module, names, cache_attr: str) -> torch.Tensor:
     return cat
 
 
+def _scaled_linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], alpha: float) -> torch.Tensor:
+    """alpha * (x @ w^T + b) as ONE library GEMM (alpha and beta in its epilogue, one rounding)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if b is None:
+        y = torch.addmm(x2.new_zeros(()), x2, w.t(), beta=0, alpha=alpha)
+    else:
+        y = torch.addmm(b, x2, w.t(), beta=alpha, alpha=alpha)
+    return y.view(*x.shape[:-1], w.shape[0])
+
+
 class CrossAttention(nn.Module):
     """diffusers 0.11.1 ``CrossAttention`` parameter layout (bias-free q/k/v, to_out = [Linear,
     Dropout]); forward = plain (un-hooked) attention on the HIP kernels."""
@@ -93,9 +103,17 @@ class FrameAttention(CrossAttention):
             x0 = (x.view(B, f, *x.shape[1:])[:, 0].contiguous() if shard.rank == 0
                   else torch.empty(B, *x.shape[1:], device=x.device, dtype=x.dtype))
             pending = (x0, shard.broadcast_async(x0))
-        q = F.linear(x, self.to_q.weight, self.to_q.bias)
+        if autograd.needs_grad(x, self.to_q.weight, self.to_q.bias):
+            q = F.linear(x, self.to_q.weight, self.to_q.bias)
+            prescaled = False
+        else:
+            # the softmax scale (times log2 e) rides in the projection GEMM's alpha: one rounding of
+            # q' = c * (x W^T + b), and K1 runs its folded-max form (frame_attn.hip)
+            q = _scaled_linear(x, self.to_q.weight, self.to_q.bias,
+                               ops.frame_query_scale(self.to_q.weight.shape[0] // self.heads, self.scale))
+            prescaled = True
         C = q.shape[-1]
-        if autograd.needs_grad(q, x):
+        if not prescaled:
             if shard is not None and shard.world > 1:
                 raise NotImplementedError("backward through frame-sharded FrameAttention (run null-text clip-parallel)")
             x0 = x.view(B, f, *x.shape[1:])[:, 0]
@@ -111,7 +129,8 @@ class FrameAttention(CrossAttention):
         else:
             x0 = x.view(B, f, *x.shape[1:])[:, 0]
         kv = F.linear(x0, wkv, bkv)
-        out = ops.frame_attention(q, kv[..., :C], kv[..., C:], f, self.heads, scale=self.scale)
+        out = ops.frame_attention(q, kv[..., :C], kv[..., C:], f, self.heads, scale=self.scale,
+                                  q_prescaled=True)
         return self.to_out[1](self.to_out[0](out))
 
 

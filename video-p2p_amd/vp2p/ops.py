@@ -58,10 +58,12 @@ def _bd_strides(t: torch.Tensor, tokens: int):
 # ----------------------------------------------------------------------------------------------
 def frame_attention(q: torch.Tensor, k0: torch.Tensor, v0: torch.Tensor, frames: int, heads: int,
                     scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
-                    lse: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    lse: Optional[torch.Tensor] = None, q_prescaled: bool = False) -> torch.Tensor:
     """FrameAttention core (attention.py:282-322).  q: (B*f, N, C); k0, v0: frame-0 keys/values
     (B, Nk, C) -- or full (B*f, Nk, C) tensors, of which only frame 0 is read.  ``lse``: optional
-    (B, heads, f*N) fp32 output of each row's log2-sum-exp2 (saved for the backward)."""
+    (B, heads, f*N) fp32 output of each row's log2-sum-exp2 (saved for the backward).
+    ``q_prescaled``: q already holds q * scale * log2(e) (see ``frame_query_scale``); K1 then runs
+    its folded-max form at head_dim 40."""
     dt = _dtype(q, k0, v0)
     Bf, N, C = q.shape
     B = Bf // frames
@@ -79,12 +81,18 @@ def frame_attention(q: torch.Tensor, k0: torch.Tensor, v0: torch.Tensor, frames:
     a = _lib.FrameAttnArgs(_ptr(q), _ptr(k0), _ptr(v0), _ptr(out), q_sb, q_sf, q_sn,
                            k_sb, k0.stride(1), v_sb, v0.stride(1), o_sb, o_sf, o_sn,
                            B, frames, N, k0.shape[1], heads, d,
-                           float(d ** -0.5 if scale is None else scale), dt, _ptr(lse))
+                           float(d ** -0.5 if scale is None else scale), dt, _ptr(lse), int(bool(q_prescaled)))
     if lse is not None and (lse.dtype != torch.float32 or not lse.is_contiguous()
                             or lse.numel() != B * heads * frames * N):
         raise ValueError("lse must be a contiguous fp32 (B, heads, f*N) tensor")
     check(_lib.load().vp2p_frame_attn_fwd(ctypes.byref(a), _stream()), "vp2p_frame_attn_fwd")
     return out
+
+
+def frame_query_scale(head_dim: int, scale: Optional[float] = None) -> float:
+    """The factor a caller folds into q for ``frame_attention(..., q_prescaled=True)``:
+    softmax scale (head_dim ** -0.5 by default) times log2(e)."""
+    return float(head_dim ** -0.5 if scale is None else scale) * 1.4426950408889634
 
 
 def frame_attention_bwd(q, k, v, o, dout, lse, frames: int, heads: int, scale: float,
