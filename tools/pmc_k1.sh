@@ -1,11 +1,11 @@
 #!/bin/bash
-# PMC passes on K1 (tools/k1_only.py) for the variants given: bash tools/pmc_k1.sh OUTDIR VAR...
+# PMC passes on K1 (tools/k1_only.py: res-64, B4 f8 d40 bf16, pre-scaled q) -> OUTDIR/{A,B,C}
+#   bash tools/pmc_k1.sh OUTDIR
 set -e
-out=$1; shift; mkdir -p $out
+out=$1; mkdir -p $out
 A="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT"
 B="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_SALU SQ_WAVES"
-for v in "$@"; do
-  for p in A B; do
-    VP2P_K1_VARIANT=$v timeout -s KILL 90 rocprofv3 --pmc ${!p} --kernel-trace --output-format csv -d $out/v${v}_$p -o run -- python3 tools/k1_only.py 5 > $out/v${v}_$p.log 2>&1
-  done
+C="SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVES SQ_WAVE_CYCLES"
+for p in A B C; do
+  timeout -s KILL 90 rocprofv3 --pmc ${!p} --kernel-trace --output-format csv -d $out/$p -o run -- python3 tools/k1_only.py 5 > $out/$p.log 2>&1
 done
