@@ -49,6 +49,20 @@ def test_conv2d(n, cin, h, w, cout, k, stride):
     _case(n, cin, h, w, cout, k, stride, residual=False)
 
 
+@pytest.mark.parametrize("n,cin,h,w,cout,k,stride,residual", [
+    (8, 320, 64, 64, 320, 3, 1, False),      # res-64 resnet conv: 256 tiles of 256 rows
+    (33, 320, 31, 33, 320, 3, 1, True),      # ragged last 256-row tile, odd sizes, residual
+    (32, 640, 32, 32, 640, 3, 1, False),     # res-32
+    (32, 320, 64, 64, 320, 3, 2, False),     # Downsample3D at res-64
+    (32, 960, 32, 32, 640, 1, 1, True),      # conv_shortcut 1x1 + residual
+    (8, 1920, 64, 64, 320, 3, 1, False),     # up-block concat input, 90 K-steps
+])
+def test_conv2d_large_m(n, cin, h, w, cout, k, stride, residual):
+    """The 256-row, three-stage LDS-DMA form (conv_kernel_p: >= 256 tiles of 256 rows) against the
+    fp32 reference at the UNet's full-size shapes."""
+    _case(n, cin, h, w, cout, k, stride, residual=residual, seed=3)
+
+
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv2d_residual(k):
     _case(2, 640, 8, 8, 640, k, 1, residual=True, seed=1)
@@ -73,7 +87,7 @@ def test_conv2d_unsupported_raises():
         ops.conv2d(x, wt, None, 1, 1)
 
 
-@pytest.mark.parametrize("M,K,inner", [(1000, 320, 1280), (257, 640, 2560), (64, 1280, 5120)])
+@pytest.mark.parametrize("M,K,inner", [(1000, 320, 1280), (257, 640, 2560), (64, 1280, 5120), (65536 + 77, 320, 1280)])
 def test_linear_geglu(M, K, inner):
     """K10 with the GEGLU epilogue vs F.linear + diffusers GEGLU in fp32 on the same bf16 inputs
     (projection rounded to bf16, gelu rounded, product rounded -- torch's eager roundings)."""
@@ -94,7 +108,7 @@ def test_linear_geglu(M, K, inner):
     assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("n,cin,h,w,cout", [(2, 1280, 8, 8, 1280), (3, 640, 5, 7, 640)])
+@pytest.mark.parametrize("n,cin,h,w,cout", [(2, 1280, 8, 8, 1280), (3, 640, 5, 7, 640), (32, 640, 32, 32, 320)])
 def test_conv2d_fused_upsample(n, cin, h, w, cout):
     """K10 reading a x2 nearest upsample on the fly == F.interpolate then the conv (fp32 reference)."""
     from vp2p import ops

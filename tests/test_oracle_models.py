@@ -16,7 +16,14 @@ from conftest import model_state
 from oracle import p2p_oracle as O
 from oracle import unet_ref
 
-torch.set_grad_enabled(False)
+
+
+@pytest.fixture(autouse=True)
+def _no_grad():
+    """Grad off inside this module's tests only (a module-level set_grad_enabled(False) would leak
+    into every test collected after it, e.g. the GPU backward tests of the same session)."""
+    with torch.no_grad():
+        yield
 
 
 @pytest.mark.parametrize("name", list(MS.FA_CONFIGS))

@@ -25,8 +25,14 @@
 //  * split-K for the small-M shapes (the 8x8 latents: 128 tiles for 256 CUs): each workgroup sums a
 //    slice of the K-steps into an fp32 workspace and a second pass adds the slices, the bias and the
 //    residual with the same roundings as the one-pass epilogue.
-// Measured (profiles/r01_conv_bench_*.jsonl): 920-960 TF/s on the large convs; register-staged
-// staging (~800), 256-row tiles and a third LDS stage (no gain) were tried and dropped.
+//  * DMA addressing: each lane's byte offset of its pixel at tap (0, 0) and a 9-bit mask of the taps
+//    that fall outside the image are computed once; a K-step's address is one add of a wave-uniform
+//    tap/channel offset, and an out-of-image tap sets bit 31 so the buffer load (raw buffer
+//    resource, num_records < 2^31) delivers the zero padding.  Rebuilding 64-bit pointers per step
+//    (~130 VALU per step per wave) was the limiter of the first form: 830-930 -> 1020-1150 TF/s.
+// Measured (profiles/r02_conv_bench_fastaddr.jsonl): 1020-1150 TF/s on the large 3x3 convs.  Tried and
+// dropped: register staging (~800), 256-row tiles with three LDS stages and a counted-vmcnt barrier
+// span (-5 %), one wave per 32 rows x 160 columns on 32x32x16 MFMAs (-9 %: every wave reads all of B).
 #include <stdlib.h>
 
 #include <type_traits>
@@ -69,7 +75,9 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 // per 160-column tile as [80 "a" rows, the 80 matching "gate" rows], and the epilogue writes
 // y[p, nt*80 + j] = a * gelu(g) (exact erf, each step rounded to bf16 as torch's eager GEGLU does)
 // into a (M, cout/2) output.  EPI = 2: split-K slice, fp32 accumulators to workspace[split].
-template <int KS, int EPI = 0>
+// FAST: 32-bit buffer offsets precomputed per DMA row (no upsample, input below 2^31 bytes): the
+// per-step address is one add + the padding mask; otherwise 64-bit pointers rebuilt per step.
+template <int KS, int EPI = 0, bool FAST = true>
 __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -106,6 +114,32 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
   int b_c[G_BDMA];
 #pragma unroll
   for (int i = 0; i < G_BDMA; ++i) b_c[i] = swz(8 * (w + NW * i) + lr, lj) * 8;
+  // FAST form: byte offsets at tap (0, 0) and the out-of-image tap masks (bit kh * KS + kw)
+  uint32_t a_off[G_ADMA], a_bad[G_ADMA], b_off[G_BDMA];
+  __amdgpu_buffer_rsrc_t xr, wr;
+  if constexpr (FAST) {
+    xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0,
+                                           (uint32_t)a.batch * a.in_h * a.in_w * a.cin * 2u, 0x00020000);
+    wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, (uint32_t)a.cout * Kw * 2u, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < G_ADMA; ++i) {
+      a_off[i] = (uint32_t)((((a_n[i] * a.in_h + a_iy[i]) * a.in_w + a_ix[i]) * a.cin + a_c[i]) * 2);
+      uint32_t bad = 0;
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          const int iy = a_iy[i] + kh, ix = a_ix[i] + kw;
+          if (!a_ok[i] || iy < 0 || iy >= a.in_h || ix < 0 || ix >= a.in_w) bad |= 1u << (kh * KS + kw);
+        }
+      a_bad[i] = bad;
+    }
+#pragma unroll
+    for (int i = 0; i < G_BDMA; ++i) {
+      const int row = 8 * (w + NW * i) + lr;
+      b_off[i] = (uint32_t)(((n0 + row) * Kw + b_c[i]) * 2);
+    }
+  }
 
   const int csteps = a.cin / BK;
   const int nall = KS * KS * csteps;
@@ -115,6 +149,19 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
     const int kh = tap / KS, kw = tap - kh * KS;
     char* As = smem + stage * G_STAGE;
     char* Bs = As + GBM * BK * 2;
+    if constexpr (FAST) {
+      const uint32_t xs = (uint32_t)(((kh * a.in_w + kw) * a.cin + c0) * 2);
+#pragma unroll
+      for (int i = 0; i < G_ADMA; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
+                                                 16, (a_off[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
+      const uint32_t ws = (uint32_t)((tap * a.cin + c0) * 2);
+#pragma unroll
+      for (int i = 0; i < G_BDMA; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)(Bs + 8 * (w + NW * i) * BK * 2),
+                                                 16, b_off[i] + ws, 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < G_ADMA; ++i) {
       const int iy = a_iy[i] + kh, ix = a_ix[i] + kw;
@@ -268,6 +315,20 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const vp2p_conv_args a
   *reinterpret_cast<bf16x8*>(static_cast<bf16*>(a.y) + o) = out;
 }
 
+template <int KS, int EPI, bool FAST>
+static int launch_g1(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, FAST>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS) == hipSuccess;
+  if (!attr) return VP2P_E_LAUNCH;
+  hipLaunchKernelGGL((conv_kernel_g<KS, EPI, FAST>), grid, dim3(256), G_LDS, s, a);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+template <int KS, int EPI>
+static int launch_g(const vp2p_conv_args& a, dim3 grid, bool fast, hipStream_t s) {
+  return fast ? launch_g1<KS, EPI, true>(a, grid, s) : launch_g1<KS, EPI, false>(a, grid, s);
+}
+
 // K-split for this shape: 1 unless the grid would leave most CUs idle (the 8x8-latent convs)
 static int pick_ksplit(const vp2p_conv_args* a) {
   if (a->epilogue != VP2P_CONV_EPI_NONE) return 1;
@@ -317,36 +378,25 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   if (M * a->cout > ((int64_t)1 << 40)) return VP2P_E_SHAPE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  static const bool attr =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<3>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<1>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<1, 1>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<3, 2>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_g<1, 2>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, conv::G_LDS) == hipSuccess;
-  if (!attr) return VP2P_E_LAUNCH;
   const int64_t tiles = (M + conv::GBM - 1) / conv::GBM * (a->cout / conv::BN);
+  const bool fast = !a->upsample && (int64_t)a->batch * a->in_h * a->in_w * a->cin * 2 < ((int64_t)1 << 31);
   int k = conv::pick_ksplit(a);
   if (k > 1 && !a->workspace) k = 1;                    // no workspace given: one pass
   if (tiles * k > 0x7fffffff) return VP2P_E_SHAPE;
-  const dim3 grid((unsigned)(tiles * k)), block(256);
+  const dim3 grid((unsigned)(tiles * k));
+  int rc;
   if (k > 1) {
     vp2p_conv_args b = *a;
     b.ksplit = k;
-    if (a->kernel == 3) hipLaunchKernelGGL((conv::conv_kernel_g<3, 2>), grid, block, conv::G_LDS, s, b);
-    else hipLaunchKernelGGL((conv::conv_kernel_g<1, 2>), grid, block, conv::G_LDS, s, b);
+    rc = a->kernel == 3 ? conv::launch_g<3, 2>(b, grid, fast, s) : conv::launch_g<1, 2>(b, grid, fast, s);
+    if (rc != VP2P_OK) return rc;
     const int64_t n = M * (a->cout / 8);
-    hipLaunchKernelGGL(conv::conv_splitk_reduce, dim3((unsigned)((n + 255) / 256)), block, 0, s, b);
+    hipLaunchKernelGGL(conv::conv_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
   } else if (a->epilogue == VP2P_CONV_EPI_GEGLU) {
-    hipLaunchKernelGGL((conv::conv_kernel_g<1, 1>), grid, block, conv::G_LDS, s, *a);
-  } else if (a->kernel == 3) {
-    hipLaunchKernelGGL((conv::conv_kernel_g<3>), grid, block, conv::G_LDS, s, *a);
+    rc = conv::launch_g<1, 1>(*a, grid, fast, s);
   } else {
-    hipLaunchKernelGGL((conv::conv_kernel_g<1>), grid, block, conv::G_LDS, s, *a);
+    rc = a->kernel == 3 ? conv::launch_g<3, 0>(*a, grid, fast, s) : conv::launch_g<1, 0>(*a, grid, fast, s);
   }
+  if (rc != VP2P_OK) return rc;
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
