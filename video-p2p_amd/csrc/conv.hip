@@ -30,7 +30,9 @@
 //    tap/channel offset, and an out-of-image tap sets bit 31 so the buffer load (raw buffer
 //    resource, num_records < 2^31) delivers the zero padding.  Rebuilding 64-bit pointers per step
 //    (~130 VALU per step per wave) was the limiter of the first form: 830-930 -> 1020-1150 TF/s.
-// Measured (profiles/r02_conv_bench_fastaddr.jsonl): 1020-1150 TF/s on the large 3x3 convs.  Tried and
+// Measured (profiles/r02_conv_bench_fastaddr.jsonl): 1020-1150 TF/s on the large 3x3 convs; the
+// Upsample3D convs on the same buffer form (AM 2): 835-964 -> 1008-1192 TF/s, bit-equal
+// (profiles/r02_conv_up_bench.jsonl).  Tried and
 // dropped: register staging (~800), 256-row tiles with three LDS stages and a counted-vmcnt barrier
 // span (-5 %), one wave per 32 rows x 160 columns on 32x32x16 MFMAs (-9 %: every wave reads all of B).
 #include <stdlib.h>
@@ -75,9 +77,12 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 // per 160-column tile as [80 "a" rows, the 80 matching "gate" rows], and the epilogue writes
 // y[p, nt*80 + j] = a * gelu(g) (exact erf, each step rounded to bf16 as torch's eager GEGLU does)
 // into a (M, cout/2) output.  EPI = 2: split-K slice, fp32 accumulators to workspace[split].
-// FAST: 32-bit buffer offsets precomputed per DMA row (no upsample, input below 2^31 bytes): the
-// per-step address is one add + the padding mask; otherwise 64-bit pointers rebuilt per step.
-template <int KS, int EPI = 0, bool FAST = true>
+// AM (addressing): 1 = 32-bit buffer offsets precomputed per DMA row (input below 2^31 bytes): the
+// per-step address is one add + the padding mask; 2 = the same with the x2 nearest upsample read on
+// the fly (per row: the source pixel's offset and the output pixel's parities; a tap's source row /
+// column step is -1, 0 or +1 by parity, two selects + adds per row and step); 0 = 64-bit pointers
+// rebuilt per step (inputs beyond 2^31 bytes).
+template <int KS, int EPI = 0, int AM = 1>
 __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -114,16 +119,23 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
   int b_c[G_BDMA];
 #pragma unroll
   for (int i = 0; i < G_BDMA; ++i) b_c[i] = swz(8 * (w + NW * i) + lr, lj) * 8;
-  // FAST form: byte offsets at tap (0, 0) and the out-of-image tap masks (bit kh * KS + kw)
+  // buffer forms: byte offsets at tap (0, 0) (AM 2: of the source pixel under the output pixel) and
+  // the out-of-image tap masks (bit kh * KS + kw; AM 2: the output pixel's parities in bits 16, 17)
   uint32_t a_off[G_ADMA], a_bad[G_ADMA], b_off[G_BDMA];
   __amdgpu_buffer_rsrc_t xr, wr;
-  if constexpr (FAST) {
+  const int sh = a.in_h >> (AM == 2), sw = a.in_w >> (AM == 2);   // stored image
+  if constexpr (AM != 0) {
     xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0,
-                                           (uint32_t)a.batch * a.in_h * a.in_w * a.cin * 2u, 0x00020000);
+                                           (uint32_t)a.batch * sh * sw * a.cin * 2u, 0x00020000);
     wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, (uint32_t)a.cout * Kw * 2u, 0x00020000);
 #pragma unroll
     for (int i = 0; i < G_ADMA; ++i) {
-      a_off[i] = (uint32_t)((((a_n[i] * a.in_h + a_iy[i]) * a.in_w + a_ix[i]) * a.cin + a_c[i]) * 2);
+      if constexpr (AM == 2) {
+        const int oy = a_iy[i] + a.pad, ox = a_ix[i] + a.pad;       // stride 1
+        a_off[i] = (uint32_t)((((a_n[i] * sh + (oy >> 1)) * sw + (ox >> 1)) * a.cin + a_c[i]) * 2);
+      } else {
+        a_off[i] = (uint32_t)((((a_n[i] * a.in_h + a_iy[i]) * a.in_w + a_ix[i]) * a.cin + a_c[i]) * 2);
+      }
       uint32_t bad = 0;
 #pragma unroll
       for (int kh = 0; kh < KS; ++kh)
@@ -132,6 +144,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
           const int iy = a_iy[i] + kh, ix = a_ix[i] + kw;
           if (!a_ok[i] || iy < 0 || iy >= a.in_h || ix < 0 || ix >= a.in_w) bad |= 1u << (kh * KS + kw);
         }
+      if constexpr (AM == 2) bad |= ((uint32_t)((a_iy[i] + a.pad) & 1) << 16) | ((uint32_t)((a_ix[i] + a.pad) & 1) << 17);
       a_bad[i] = bad;
     }
 #pragma unroll
@@ -149,12 +162,26 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
     const int kh = tap / KS, kw = tap - kh * KS;
     char* As = smem + stage * G_STAGE;
     char* Bs = As + GBM * BK * 2;
-    if constexpr (FAST) {
-      const uint32_t xs = (uint32_t)(((kh * a.in_w + kw) * a.cin + c0) * 2);
+    if constexpr (AM != 0) {
+      if constexpr (AM == 2) {
+        // source row step of tap row kh for output-row parity py: kh 0 -> py - 1, 1 -> 0, 2 -> py
+        const uint32_t rs = (uint32_t)(sw * a.cin * 2), cs = (uint32_t)(a.cin * 2);
+        const uint32_t ry0 = kh == 0 ? 0u - rs : 0u, ry1 = kh == 2 ? rs : 0u;
+        const uint32_t cx0 = kw == 0 ? 0u - cs : 0u, cx1 = kw == 2 ? cs : 0u;
+        const uint32_t xs = (uint32_t)(c0 * 2);
 #pragma unroll
-      for (int i = 0; i < G_ADMA; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
-                                                 16, (a_off[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
+        for (int i = 0; i < G_ADMA; ++i) {
+          const uint32_t o = a_off[i] + xs + ((a_bad[i] >> 16) & 1 ? ry1 : ry0) + ((a_bad[i] >> 17) & 1 ? cx1 : cx0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
+                                                   16, o | ((a_bad[i] >> tap) << 31), 0, 0, 0);
+        }
+      } else {
+        const uint32_t xs = (uint32_t)(((kh * a.in_w + kw) * a.cin + c0) * 2);
+#pragma unroll
+        for (int i = 0; i < G_ADMA; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
+                                                   16, (a_off[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
+      }
       const uint32_t ws = (uint32_t)((tap * a.cin + c0) * 2);
 #pragma unroll
       for (int i = 0; i < G_BDMA; ++i)
@@ -315,18 +342,21 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const vp2p_conv_args a
   *reinterpret_cast<bf16x8*>(static_cast<bf16*>(a.y) + o) = out;
 }
 
-template <int KS, int EPI, bool FAST>
+template <int KS, int EPI, int AM>
 static int launch_g1(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, FAST>),
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, AM>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  hipLaunchKernelGGL((conv_kernel_g<KS, EPI, FAST>), grid, dim3(256), G_LDS, s, a);
+  hipLaunchKernelGGL((conv_kernel_g<KS, EPI, AM>), grid, dim3(256), G_LDS, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
+// am: addressing form (see conv_kernel_g); the upsampling form exists for the 3x3 one-pass kernel only
 template <int KS, int EPI>
-static int launch_g(const vp2p_conv_args& a, dim3 grid, bool fast, hipStream_t s) {
-  return fast ? launch_g1<KS, EPI, true>(a, grid, s) : launch_g1<KS, EPI, false>(a, grid, s);
+static int launch_g(const vp2p_conv_args& a, dim3 grid, int am, hipStream_t s) {
+  if constexpr (KS == 3 && EPI == 0)
+    if (am == 2) return launch_g1<KS, EPI, 2>(a, grid, s);
+  return am == 1 ? launch_g1<KS, EPI, 1>(a, grid, s) : launch_g1<KS, EPI, 0>(a, grid, s);
 }
 
 // K-split for this shape: 1 unless the grid would leave most CUs idle (the 8x8-latent convs)
@@ -379,9 +409,14 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   if (M * a->cout > ((int64_t)1 << 40)) return VP2P_E_SHAPE;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t tiles = (M + conv::GBM - 1) / conv::GBM * (a->cout / conv::BN);
-  const bool fast = !a->upsample && (int64_t)a->batch * a->in_h * a->in_w * a->cin * 2 < ((int64_t)1 << 31);
   int k = conv::pick_ksplit(a);
   if (k > 1 && !a->workspace) k = 1;                    // no workspace given: one pass
+  // addressing: 32-bit buffer offsets when the stored input is below 2^31 bytes (the upsampling
+  // form for the one-pass 3x3 kernel), 64-bit pointers otherwise
+  const int64_t in_bytes = (int64_t)a->batch * (a->in_h >> a->upsample) * (a->in_w >> a->upsample) * a->cin * 2;
+  const int fast = in_bytes >= ((int64_t)1 << 31) ? 0
+                   : !a->upsample ? 1
+                   : (a->kernel == 3 && k == 1 && a->epilogue == VP2P_CONV_EPI_NONE) ? 2 : 0;
   if (tiles * k > 0x7fffffff) return VP2P_E_SHAPE;
   const dim3 grid((unsigned)(tiles * k));
   int rc;

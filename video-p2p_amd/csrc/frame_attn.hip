@@ -21,7 +21,8 @@
 //        so O is rarely touched; P <= 2^kRescaleThr in between (bf16-safe, fp32 accumulators),
 //      - masking only on the ragged last tile.
 //  * next K/V tile prefetched into registers while the current one is consumed
-//    (issue early / write late); two barriers per 128-key tile.
+//    (issue early / write late); two barriers per 128-key tile (the folded d = 40 form: two LDS
+//    tiles and one barrier per tile).
 //  * bf16, d <= 80 (the res-64 and res-32 layers, 98% of the FLOPs): frame_attn_kernel_x2f gives
 //    every wave 64 query rows as two independent 32-row sets sharing each K/V fragment read (half
 //    the LDS traffic per query, two independent MFMA/VALU chains per wave) -- see its header.
@@ -284,6 +285,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
 // ------------------------------------------------------------------------------------------------
 constexpr float kSumThr = 4096.f;
 
+
 // Exact two-pass softmax row of one query in plain fp32 VALU (the overflow fallback of x2f):
 // writes this lane's epilogue slots of the output row and the row's log-sum-exp.
 // Small register footprint (the query row is re-read from memory, one 4-column output slot
@@ -335,8 +337,14 @@ __device__ __forceinline__ void frame_attn_exact_row(const vp2p_frame_attn_args&
 //                 block j and set 0's QK^T of block j + 1 are issued ahead of the other set's softmax,
 //                 so each set's exp/cvt run under MFMAs (128-key tiles keep the extra score registers
 //                 within the 2-waves/SIMD budget).
+// LDS tiles of x2f: two for the folded d = 40 form (tile t+1 is stored from registers while tile t
+// is consumed: one barrier per key tile instead of two; 77.8 KB, two workgroups per CU: 0.813 ->
+// 0.800 ms at res-64, profiles/r02_k1_lab_q.jsonl), one elsewhere (d = 80 spills with two).
+constexpr int x2f_bufs(int D, int KT, bool FOLD) { return FOLD && D <= 64 && KT <= 128 ? 2 : 1; }
+
 template <int D, int KT, bool FOLD>
 __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame_attn_args a) {
+  constexpr int kK1Bufs = x2f_bufs(D, KT, FOLD);
   using T = bf16;
   using M = Mfma<T>;
   using C = FrameCfg<T, D>;
@@ -345,7 +353,8 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   constexpr int PAD_S = D / 16, PAD_H = (D % 16) / 8, PAD_J = D % 8;   // qf slot of column D
   constexpr int NBLK = KT / 32;
   constexpr int NCH = (KT * C::CPR + 255) / 256;          // 16-byte chunks per thread per tile
-  constexpr int LDS_BYTES = KT * (C::KROW + C::VROW) * 2;
+  constexpr int TILE_BYTES = KT * (C::KROW + C::VROW) * 2;
+  constexpr int LDS_BYTES = kK1Bufs * TILE_BYTES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Ks = reinterpret_cast<T*>(smem);
   T* Vs = Ks + KT * C::KROW;
@@ -373,9 +382,11 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   }
   for (int i = tid; i < LDS_BYTES / 16; i += 256) reinterpret_cast<u32x4*>(smem)[i] = u32x4{0, 0, 0, 0};
   __syncthreads();
-  for (int k = tid; k < KT; k += 256) {
-    Vs[k * C::VROW + D] = (T)1.0f;                 // O^T row D = sum_k p
-    if constexpr (FOLD) Ks[k * C::KROW + D] = (T)1.0f;   // S^T += 1 * Q'[D] = -m
+  for (int k = tid; k < kK1Bufs * KT; k += 256) {
+    const int bi = k / KT, kk = k - bi * KT;
+    T* kb_ = reinterpret_cast<T*>(smem + bi * TILE_BYTES);
+    kb_[KT * C::KROW + kk * C::VROW + D] = (T)1.0f;     // O^T row D = sum_k p
+    if constexpr (FOLD) kb_[kk * C::KROW + D] = (T)1.0f; // S^T += 1 * Q'[D] = -m
   }
 
   const T* kbase = static_cast<const T*>(a.k) + b * a.k_sb + head * D;
@@ -396,14 +407,16 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
       }
     }
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](int buf) {
+    T* kd = reinterpret_cast<T*>(smem + buf * TILE_BYTES);
+    T* vd = kd + KT * C::KROW;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = tid + i * 256;
       if (c < KT * C::CPR) {
         const int row = c / C::CPR, col = (c - row * C::CPR) * C::EPC;
-        *reinterpret_cast<u32x4*>(Ks + row * C::KROW + col) = kreg[i];
-        *reinterpret_cast<u32x4*>(Vs + row * C::VROW + col) = vreg[i];
+        *reinterpret_cast<u32x4*>(kd + row * C::KROW + col) = kreg[i];
+        *reinterpret_cast<u32x4*>(vd + row * C::VROW + col) = vreg[i];
       }
     }
   };
@@ -531,21 +544,48 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   };
 
   load_tile(0);
-  int kt = 0;
-  for (; kt + KT <= Nk; kt += KT) {
+  if constexpr (kK1Bufs == 2) {
+    // two LDS tiles: tile t+1 is stored (from registers loaded during tile t-1) while tile t is
+    // consumed, and one barrier per tile both publishes it and retires the reads of tile t-1
     __syncthreads();
-    store_tile();
+    store_tile(0);
     __syncthreads();
-    if (kt + KT < Nk) load_tile(kt + KT);
-    if (kt == 0) init_max();
-    compute_tile(kt, std::false_type{});
-  }
-  if (kt < Nk) {
-    __syncthreads();
-    store_tile();
-    __syncthreads();
-    if (kt == 0) init_max();
-    compute_tile(kt, std::true_type{});
+    if (KT < Nk) load_tile(KT);
+    init_max();
+    int it = 0, kt = 0;
+    for (; kt + KT <= Nk; kt += KT, ++it) {
+      const int cur = it & 1;
+      Ks = reinterpret_cast<T*>(smem + cur * TILE_BYTES);
+      Vs = Ks + KT * C::KROW;
+      compute_tile(kt, std::false_type{});
+      if (kt + KT < Nk) {
+        store_tile(cur ^ 1);
+        if (kt + 2 * KT < Nk) load_tile(kt + 2 * KT);
+        __syncthreads();
+      }
+    }
+    if (kt < Nk) {
+      Ks = reinterpret_cast<T*>(smem + (it & 1) * TILE_BYTES);
+      Vs = Ks + KT * C::KROW;
+      compute_tile(kt, std::true_type{});
+    }
+  } else {
+    int kt = 0;
+    for (; kt + KT <= Nk; kt += KT) {
+      __syncthreads();
+      store_tile(0);
+      __syncthreads();
+      if (kt + KT < Nk) load_tile(kt + KT);
+      if (kt == 0) init_max();
+      compute_tile(kt, std::false_type{});
+    }
+    if (kt < Nk) {
+      __syncthreads();
+      store_tile(0);
+      __syncthreads();
+      if (kt == 0) init_max();
+      compute_tile(kt, std::true_type{});
+    }
   }
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
@@ -591,7 +631,7 @@ static bool x2f_d80_off() {   // VP2P_K1_D80=1set: A/B switch for the res-32 lay
 
 template <int D, int KT, bool FOLD>
 static int launch_x2f(const vp2p_frame_attn_args* a, int64_t nwg, hipStream_t stream) {
-  constexpr int lds = KT * (FrameCfg<bf16, D>::KROW + FrameCfg<bf16, D>::VROW) * 2;
+  constexpr int lds = x2f_bufs(D, KT, FOLD) * KT * (FrameCfg<bf16, D>::KROW + FrameCfg<bf16, D>::VROW) * 2;
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_x2f<D, KT, FOLD>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
