@@ -161,10 +161,13 @@ def _plan(ctrl, lb_alpha=None):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("name,step", [("rabbit", 0), ("rabbit", 12), ("car", 3), ("man", 5), ("bird", 30)])
-def test_cross_attention_p2p(tokenizer, dtype, name, step):
+@pytest.mark.parametrize("name,step,d", [("rabbit", 0, 40), ("rabbit", 12, 40), ("car", 3, 40), ("man", 5, 40),
+                                         ("bird", 30, 40), ("rabbit", 12, 160), ("bird", 30, 80), ("car", 20, 160)])
+def test_cross_attention_p2p(tokenizer, dtype, name, step, d):
+    """Edit launches (inside the cross-replace window) and non-edit launches (K2 v3: K/V in LDS) at
+    the UNet's head dims, with LocalBlend sums and stored maps."""
     from vp2p import ops
-    heads, P, frames, n, d = 8, 2, 2, 256, 40
+    heads, P, frames, n = 8, 2, 2, 256
     B, C = 2 * P, heads * d
     ctrl = _controller(tokenizer, name, step)
     lb_alpha = ctrl.local_blend.alpha_layers.reshape(P, 77) if ctrl.local_blend else np.ones((P, 77), np.float32)
@@ -178,8 +181,11 @@ def test_cross_attention_p2p(tokenizer, dtype, name, step):
     plan = _plan(ctrl, lb_alpha)
     lb_acc = torch.zeros(P, frames, n, device=DEV)
     probs = torch.empty(B * frames * heads, n, 77, device=DEV)
+    # the flag the fused protocol passes (controllers.fused_begin): edit launches only inside the
+    # cross-replace window (outside it the reference edits nothing, Reweight included)
+    edit = bool(ctrl.cross_replace_alpha.reshape(ctrl.cross_replace_alpha.shape[0], -1)[step].max() > 0)
     out = ops.cross_attention_p2p(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, plan=plan, step=step,
-                                  lb_acc=lb_acc, probs_out=probs)
+                                  edit=edit, lb_acc=lb_acc, probs_out=probs)
     torch.cuda.synchronize()
     tol = TOL[dtype]
     assert _rel(probs.cpu().numpy(), ref_p) < tol, _rel(probs.cpu().numpy(), ref_p)
@@ -190,10 +196,11 @@ def test_cross_attention_p2p(tokenizer, dtype, name, step):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_cross_attention_plain(dtype):
+@pytest.mark.parametrize("d", [40, 80, 160])
+def test_cross_attention_plain(dtype, d):
     """No controller: plain hooked softmax-attention (DummyController, ptp_utils.py:225-234)."""
     from vp2p import ops
-    heads, frames, n, d, B = 8, 3, 100, 80, 3
+    heads, frames, n, B = 8, 3, 100, 3
     C = heads * d
     q = _rand((B * frames, n, C), 10, 1.0, dtype)
     k = _rand((B, 77, C), 11, 1.0, dtype)

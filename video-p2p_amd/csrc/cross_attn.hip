@@ -329,67 +329,77 @@ void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// K2 v2 (bf16, d <= 64): the launches WITHOUT an edit (every uncond half, and the cond half outside
-// the cross-replace window: 40 of the 50 steps), with K/V in REGISTERS and persistent waves.
+// K2 v3 (bf16, any head dim): the launches WITHOUT an edit, K/V of one (batch row, head) in LDS.
 //
-// The 77-key K/V of one (batch row, head) is the same for every query block, so each wave loads its
-// row's K fragments (KB x KS) and V^T fragments (NT x KB x 2) once and then streams query blocks:
-// per block only Q (prefetched one block ahead) comes in and O goes out -- the HBM traffic the
-// roofline counts -- with no K/V re-reads through L2 per block (the v1 kernel's 21 KB per wave and
-// prompt) and no per-block dependency on a K/V fetch.  Wave w runs prompt (w & 1) of query stream
-// (w >> 1) of a CFG half (two prompts), or stream w of a plain batch row.  Softmax normalisation
-// moves to O (flash-style) unless something reads the probabilities (LocalBlend sum, stored maps).
+// A workgroup is one (batch row, head): its 4 waves are 4 query streams that share the row's K and
+// V^T fragments, staged once from the prepared workspace into padded LDS rows (row strides of 4
+// (mod 8) dwords: the 16-lane groups of a ds_read_b128 hit distinct banks).  With the fragments in
+// LDS instead of registers (round-2 v2 kept them in VGPRs, d <= 64 only) and one 32-column output
+// tile live at a time, a wave needs ~100 (d 40) / ~135 (d 80) VGPRs: 3-4 waves per SIMD hide the
+// per-block Q -> QK^T -> softmax -> PV -> O chain and the Q fetch.  Per block only Q (prefetched one
+// block ahead) comes in and O goes out.  Measured (profiles/r02_k2_v3_ab.jsonl, non-edit launches,
+// B4 f8): res-64 d 40 54.9 (v2) -> 53.9 us, res-32 d 80 62.0 (v1) -> 39.5, res-16 d 160 37.4 -> 26.5.
 // ------------------------------------------------------------------------------------------------
 template <int D, int KB>
-__global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_attn_args a, int iters) {
+struct CrossV3Cfg {
+  using C = CrossCfg<bf16, D>;
+  static constexpr int KP = 32 * KB;
+  static constexpr int KROW = C::DP + 8;          // K rows (keys) in LDS
+  static constexpr int VROW = KP + 8;             // V^T rows (head columns) in LDS
+  static constexpr int LDS = (KP * KROW + C::DV * VROW) * 2;
+};
+
+template <int D, int KB>
+__global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(const vp2p_cross_attn_args a, int iters) {
   using T = bf16;
   using M = Mfma<T>;
   using C = CrossCfg<T, D>;
-  constexpr int KP = 32 * KB;
+  using V3 = CrossV3Cfg<D, KB>;
+  constexpr int KP = V3::KP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Ks = reinterpret_cast<T*>(smem);
+  T* Vs = Ks + KP * V3::KROW;
+  float* lbw = reinterpret_cast<float*>(smem + V3::LDS);   // [sets][NKV] of this row's prompt
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int FQ = a.frames * a.tokens_q;
-  const int qblocks = (FQ + 31) >> 5;
-  const bool p2p = a.prompts == 2 && a.batch == (a.cond_only ? 1 : 2) * a.prompts;
-  const int g = blockIdx.y;                    // CFG half (p2p) or batch row
+  const bool p2p = a.prompts > 0 && a.batch == (a.cond_only ? 1 : 2) * a.prompts;
+  const int b = blockIdx.y;                     // batch row
   const int head = blockIdx.z;
+  const int g = p2p ? b / a.prompts : 0;        // CFG half
+  const int pw = p2p ? b - g * a.prompts : 0;   // prompt within the half
   const bool cond = p2p && (a.cond_only || g == 1);
   const bool lb = cond && a.lb_acc != nullptr;
   const int NKV = a.tokens_kv;
-  const int pw = p2p ? (w & 1) : 0;
-  const int sw = p2p ? (w >> 1) : w;
-  const int NS = p2p ? 2 : 4;
-  const int b = p2p ? g * 2 + pw : g;          // batch row of this wave
-
-  float* lbw = reinterpret_cast<float*>(smem);  // [sets][2][NKV]
   const int LBS = a.lb_sets == 2 ? 2 : 1;
-  if (lb) {
-    for (int i = tid; i < LBS * 2 * NKV; i += 256) lbw[i] = a.lb_word_alpha[i];
-    __syncthreads();
-  }
 
+  // stage this (row, head)'s K [KP][DP] and V^T [DV][KP] fragments (16-byte vectors)
   const T* ws = static_cast<const T*>(a.kv_ws);
   const int64_t kelems = (int64_t)a.batch * a.heads * KP * C::DP;
   const T* kb_base = ws + ((int64_t)(b * a.heads + head) * KP) * C::DP;
   const T* vb_base = ws + kelems + ((int64_t)(b * a.heads + head) * KP) * C::DV;
-  bf16x8 kf[KB][C::KS], vf[KB][2][C::NT];
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s)
-      kf[kb][s] = *reinterpret_cast<const bf16x8*>(kb_base + (kb * 32 + r) * C::DP + 16 * s + 8 * h);
-#pragma unroll
-    for (int sp = 0; sp < 2; ++sp)
-#pragma unroll
-      for (int t = 0; t < C::NT; ++t)
-        vf[kb][sp][t] = *reinterpret_cast<const bf16x8*>(vb_base + (int64_t)(32 * t + r) * KP + kb * 32 + 16 * sp + 8 * h);
+  constexpr int KV8 = KP * C::DP / 8, VV8 = C::DV * KP / 8;
+  for (int i = tid; i < KV8 + VV8; i += 256) {
+    if (i < KV8) {
+      const int row = i / (C::DP / 8), c = (i - row * (C::DP / 8)) * 8;
+      *reinterpret_cast<u32x4*>(Ks + row * V3::KROW + c) = *reinterpret_cast<const u32x4*>(kb_base + row * C::DP + c);
+    } else {
+      const int j = i - KV8, row = j / (KP / 8), c = (j - row * (KP / 8)) * 8;
+      *reinterpret_cast<u32x4*>(Vs + row * V3::VROW + c) = *reinterpret_cast<const u32x4*>(vb_base + row * KP + c);
+    }
   }
+  if (lb)
+    for (int i = tid; i < LBS * NKV; i += 256) {
+      const int set = i / NKV, wd = i - set * NKV;
+      lbw[i] = a.lb_word_alpha[(set * a.prompts + pw) * NKV + wd];
+    }
+  __syncthreads();
 
   const float cs = a.scale * kLog2e;
   const bool norm_p = lb || a.probs_out;
-  // this stream's query blocks: qb0, qb0 + NS, ...; (frame, token) of the lane's query tracked
+  // stream w's query blocks: qb0, qb0 + 4, ...; (frame, token) of the lane's query tracked
   // incrementally (no integer division in the loop)
-  const int qb0 = blockIdx.x * NS * iters + sw;
+  const int qb0 = blockIdx.x * 4 * iters + w;
+  constexpr int NS = 4;
   const int step = 32 * NS;
   const T* qbase = static_cast<const T*>(a.q) + b * a.q_sb + head * D;
   T* obase = static_cast<T*>(a.o) + b * a.o_sb + head * D;
@@ -415,7 +425,7 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
     for (int s = 0; s < C::KS; ++s) qf[s] = qn[s];
     const int qcur = qi;
     const int fcur = fr_n, pcur = pos_n;
-    if (it + 1 < iters) {        // next block's Q (prefetching two ahead measured slower: 60 vs 56 us)
+    if (it + 1 < iters) {
       advance(fr_n, pos_n);
       qi += step;
       load_q(qi, fr_n, pos_n, qn);
@@ -427,7 +437,9 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
     for (int kb = 0; kb < KB; ++kb) {
       sc[kb] = zero16();
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s) sc[kb] = M::mma(kf[kb][s], qf[s], sc[kb]);
+      for (int s = 0; s < C::KS; ++s)
+        sc[kb] = M::mma(*reinterpret_cast<const bf16x8*>(Ks + (kb * 32 + r) * V3::KROW + 16 * s + 8 * h), qf[s], sc[kb]);
+      __builtin_amdgcn_sched_barrier(0);      // no hoisting of every block's K fragments at once
     }
     // row softmax: only the last key block is ragged; max on raw scores, exp2(s*cs - max*cs) fused
     float mx = kNegInf;
@@ -457,7 +469,7 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
         for (int i = 0; i < 16; ++i) sc[kb][i] *= inv;
       if (lb) {  // this head's word-weighted map of token qi -> lb_ws[set][p][head][qi]
         for (int set = 0; set < LBS; ++set) {
-          const float* wts = lbw + (set * 2 + pw) * NKV;
+          const float* wts = lbw + set * NKV;
           float part = 0.f;
 #pragma unroll
           for (int kb = 0; kb < KB; ++kb)
@@ -467,7 +479,7 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
               if (wd < NKV) part += wts[wd] * sc[kb][i];
             }
           part += xhalf(part);
-          if (h == 0 && qv) a.lb_ws[((int64_t)(set * 2 + pw) * a.heads + head) * FQ + qcur] = part;
+          if (h == 0 && qv) a.lb_ws[((int64_t)(set * a.prompts + pw) * a.heads + head) * FQ + qcur] = part;
         }
       }
       if (a.probs_out && qv) {
@@ -482,31 +494,36 @@ __global__ __launch_bounds__(256, 2) void cross_attn_kernel_v2(const vp2p_cross_
       }
     }
     const float oscale = norm_p ? 1.f : inv;
-    f32x16 o[C::NT];
+    // P as bf16 B fragments (the fp32 scores die here), then one 32-column output tile at a time:
+    // only 16 accumulators live, which keeps d = 80 / 160 within the register budget
+    bf16x8 pf[KB][2];
 #pragma unroll
-    for (int t = 0; t < C::NT; ++t) o[t] = zero16();
+    for (int kb = 0; kb < KB; ++kb) {
+      pf[kb][0] = M::p_frag(sc[kb], 0);
+      pf[kb][1] = M::p_frag(sc[kb], 1);
+    }
+    T* orow = obase + fcur * a.o_sf + pcur * a.o_sn;
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
+    for (int t = 0; t < C::NT; ++t) {
+      f32x16 o = zero16();
 #pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        const bf16x8 pf = M::p_frag(sc[kb], sp);
+      for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int t = 0; t < C::NT; ++t) o[t] = M::mma(vf[kb][sp][t], pf, o[t]);
-      }
-    if (qv) {
-      T* orow = obase + fcur * a.o_sf + pcur * a.o_sn;
-#pragma unroll
-      for (int t = 0; t < C::NT; ++t)
+        for (int sp = 0; sp < 2; ++sp)
+          o = M::mma(*reinterpret_cast<const bf16x8*>(Vs + (32 * t + r) * V3::VROW + kb * 32 + 16 * sp + 8 * h), pf[kb][sp], o);
+      __builtin_amdgcn_sched_barrier(0);
+      if (qv) {
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
           const int dc = 32 * t + 8 * gq + 4 * h;
           if (dc < D) {
             bf16x4 v;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[t][4 * gq + j] * oscale);
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[4 * gq + j] * oscale);
             *reinterpret_cast<bf16x4*>(orow + dc) = v;
           }
         }
+      }
     }
   }
 }
@@ -543,37 +560,37 @@ static int cross_pad_dims(int head_dim, int dtype, int& dp, int& dv) {
 #undef VP2P_DIMS
 }
 
-static int cross_v2_disabled() {   // VP2P_K2=v1: A/B switch, read once
-  static const int off = [] {
+// VP2P_K2=v1: A/B switch for the non-edit launches (default v3), read once
+static int cross_nonedit_kernel() {
+  static const int k = [] {
     const char* e = getenv("VP2P_K2");
-    return (e && e[0] == 'v' && e[1] == '1') ? 1 : 0;
+    return (e && e[0] == 'v' && e[1] == '1') ? 1 : 3;
   }();
-  return off;
+  return k;
 }
 
 template <typename T, int D, int KB>
 static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
   const int FQ = a->frames * a->tokens_q;
-  if constexpr (sizeof(T) == 2 && D <= 64) {
+  if constexpr (sizeof(T) == 2) {
     const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
-    // edit launches (the first int(cross_replace * 51) steps) keep v1: its one-wave-per-item walk over
-    // both prompts needs no cross-wave exchange of the source probabilities (v2's pair barrier
-    // measured slower there: 163 vs 129 us at res-64)
     const bool edit = p2p && (a->edit_mode != VP2P_EDIT_NONE || a->reweight);
-    if ((!p2p || a->prompts == 2) && !edit && !cross_v2_disabled()) {
-      const int groups = p2p ? (a->cond_only ? 1 : 2) : a->batch;
-      const int NS = p2p ? 2 : 4;
+    if (!edit && cross_nonedit_kernel() == 3) {
+      using V3 = CrossV3Cfg<D, KB>;
       const int64_t qblocks = (FQ + 31) / 32;
-      const int64_t per_group = (qblocks + NS - 1) / NS;          // iterations of one stream, all blocks
-      // enough workgroups for ~2 per CU over the (group, head) grid; each stream then loops `iters`
-      const int64_t gh = (int64_t)groups * a->heads;
-      int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_group, (512 + gh - 1) / gh));
-      const int iters = (int)((per_group + nx - 1) / nx);
-      nx = (per_group + iters - 1) / iters;
-      if (gh > 65535 * 64 || nx > 0x7fffffff) return VP2P_E_SHAPE;
+      const int64_t per_wg = (qblocks + 3) / 4;                 // iterations of one stream, all blocks
+      const int64_t gh = (int64_t)a->batch * a->heads;
+      // ~4 workgroups per CU over the (row, head) grid; each stream then loops `iters` blocks
+      int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (1024 + gh - 1) / gh));
+      const int iters = (int)((per_wg + nx - 1) / nx);
+      nx = (per_wg + iters - 1) / iters;
+      if (a->batch > 65535 || a->heads > 65535 || nx > 0x7fffffff) return VP2P_E_SHAPE;
       const int sets = a->lb_sets == 2 ? 2 : 1;
-      const size_t lds = (size_t)sets * 2 * a->tokens_kv * sizeof(float);
-      hipLaunchKernelGGL((cross_attn_kernel_v2<D, KB>), dim3((unsigned)nx, (unsigned)groups, (unsigned)a->heads),
+      const size_t lds = (size_t)V3::LDS + (size_t)sets * a->tokens_kv * sizeof(float);
+      static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+      if (!attr || lds > 160 * 1024) return VP2P_E_LAUNCH;
+      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB>), dim3((unsigned)nx, (unsigned)a->batch, (unsigned)a->heads),
                          dim3(256), lds, s, *a, iters);
       if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
       if (p2p && a->lb_acc) {
