@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 8
+#define VP2P_ABI_VERSION 9
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -262,7 +262,14 @@ int vp2p_group_norm_stats(const vp2p_group_norm_args* args, void* stream);
 /* nsets partial arrays laid out back to back, each (batch, parts, groups, 3) */
 int vp2p_group_norm_apply(const vp2p_group_norm_args* args, const float* partials, int32_t nsets,
                           void* stream);
-int vp2p_group_norm_fwd(const vp2p_group_norm_args* args, void* stream);   /* stats + apply */
+int vp2p_group_norm_fwd(const vp2p_group_norm_args* args, void* stream);   /* stats + finalize + apply */
+/* Merge the nsets partial arrays once into per-(batch, group) {mean, rstd} fp32 (batch, groups, 2)
+ * (resnet.py:142,158: nn.GroupNorm's statistics over c/G x f x h x w), so that the apply blocks read
+ * two floats per group instead of each merging every partial. */
+int vp2p_group_norm_finalize(const vp2p_group_norm_args* args, const float* partials, int32_t nsets,
+                             float* stats, void* stream);
+/* The apply of vp2p_group_norm_apply on finalized statistics. */
+int vp2p_group_norm_apply_stats(const vp2p_group_norm_args* args, const float* stats, void* stream);
 
 /* ---- K8: LayerNorm over the channel axis --------------------------------------------------------
  * nn.LayerNorm of BasicTransformerBlock.norm1/norm2/norm3/norm_temp (attention.py:200-216). */

@@ -195,36 +195,78 @@ __global__ __launch_bounds__(512) void gn_stats_kernel(const vp2p_group_norm_arg
   }
 }
 
-template <typename T, bool ADD, bool SILU>
+// Finalize: one 256-thread block per (group, batch element) merges that group's nsets x parts
+// partials -- one load per thread in flight, then a fixed-order tree in LDS -- into {mean, rstd}.
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const vp2p_group_norm_args a, const GnGeom g,
+                                                          const float* __restrict__ partials, int nsets,
+                                                          float* __restrict__ stats) {
+  __shared__ float s_n[256], s_mean[256], s_m2[256];
+  const int G = a.groups, gi = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int total = nsets * g.parts;
+  Welford w = {0.f, 0.f, 0.f};
+  for (int e = tid; e < total; e += 256) {
+    const int set = e / g.parts, p = e - set * g.parts;
+    const float* q = partials + ((((int64_t)set * a.batch + b) * g.parts + p) * G + gi) * 3;
+    w = wmerge(w, {q[0], q[1], q[2]});
+  }
+  s_n[tid] = w.n;
+  s_mean[tid] = w.mean;
+  s_m2[tid] = w.m2;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) {
+      const Welford t = wmerge({s_n[tid], s_mean[tid], s_m2[tid]}, {s_n[tid + st], s_mean[tid + st], s_m2[tid + st]});
+      s_n[tid] = t.n;
+      s_mean[tid] = t.mean;
+      s_m2[tid] = t.m2;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    stats[((int64_t)b * G + gi) * 2] = s_mean[0];
+    stats[((int64_t)b * G + gi) * 2 + 1] = rsqrtf(s_m2[0] / s_n[0] + a.eps);
+  }
+}
+
+// FIN: statistics already finalized (`stats`, (batch, groups, 2)); otherwise every block merges all
+// partials itself (the ABI's vp2p_group_norm_apply)
+template <typename T, bool ADD, bool SILU, bool FIN = false>
 __global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_args a, const GnGeom g,
                                                         const float* __restrict__ partials, int nsets) {
-  __shared__ float s_w[3 * 512];
+  __shared__ float s_w[FIN ? 1 : 3 * 512];
   __shared__ float s_mean[64], s_rstd[64];
   const int C = a.channels, G = a.groups, R = g.R, nvec = g.nvec, cg = g.cg;
   const int b = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
-  const int tpg = g.threads / G;
-  const int gi = tid / tpg, k = tid - gi * tpg;
-  Welford w = {0.f, 0.f, 0.f};
-  if (gi < G) {
-    const int total = nsets * g.parts;
-    for (int e = k; e < total; e += tpg) {
-      const int set = e / g.parts, p = e - set * g.parts;
-      const float* q = partials + ((((int64_t)set * a.batch + b) * g.parts + p) * G + gi) * 3;
-      w = wmerge(w, {q[0], q[1], q[2]});
+  if constexpr (FIN) {
+    if (tid < G) {
+      s_mean[tid] = partials[((int64_t)b * G + tid) * 2];
+      s_rstd[tid] = partials[((int64_t)b * G + tid) * 2 + 1];
     }
-  }
-  s_w[tid] = w.n;
-  s_w[512 + tid] = w.mean;
-  s_w[1024 + tid] = w.m2;
-  __syncthreads();
-  if (tid < G) {
-    Welford t = {0.f, 0.f, 0.f};
-    for (int e = 0; e < tpg; ++e) {
-      const int i = tid * tpg + e;
-      t = wmerge(t, {s_w[i], s_w[512 + i], s_w[1024 + i]});
+  } else {
+    const int tpg = g.threads / G;
+    const int gi = tid / tpg, k = tid - gi * tpg;
+    Welford w = {0.f, 0.f, 0.f};
+    if (gi < G) {
+      const int total = nsets * g.parts;
+      for (int e = k; e < total; e += tpg) {
+        const int set = e / g.parts, p = e - set * g.parts;
+        const float* q = partials + ((((int64_t)set * a.batch + b) * g.parts + p) * G + gi) * 3;
+        w = wmerge(w, {q[0], q[1], q[2]});
+      }
     }
-    s_mean[tid] = t.mean;
-    s_rstd[tid] = rsqrtf(t.m2 / t.n + a.eps);
+    s_w[tid] = w.n;
+    s_w[512 + tid] = w.mean;
+    s_w[1024 + tid] = w.m2;
+    __syncthreads();
+    if (tid < G) {
+      Welford t = {0.f, 0.f, 0.f};
+      for (int e = 0; e < tpg; ++e) {
+        const int i = tid * tpg + e;
+        t = wmerge(t, {s_w[i], s_w[512 + i], s_w[1024 + i]});
+      }
+      s_mean[tid] = t.mean;
+      s_rstd[tid] = rsqrtf(t.m2 / t.n + a.eps);
+    }
   }
   __syncthreads();
   const int v = tid % nvec, r = tid / nvec;
@@ -286,15 +328,16 @@ static void gn_stats_launch(const vp2p_group_norm_args& a, const GnGeom& g, hipS
     hipLaunchKernelGGL((gn_stats_kernel<T, false>), grid, dim3(g.threads), lds, s, a, g);
 }
 
-template <typename T>
+// parts = the partial sets (FIN = false) or the finalized (batch, groups, 2) statistics (FIN = true)
+template <typename T, bool FIN = false>
 static void gn_apply_launch(const vp2p_group_norm_args& a, const GnGeom& g, const float* parts, int nsets,
                             hipStream_t s) {
   const dim3 grid(g.parts, a.batch), block(g.threads);
   const bool add = a.add != nullptr, silu = a.silu != 0;
-  if (add && silu) hipLaunchKernelGGL((gn_apply_kernel<T, true, true>), grid, block, 0, s, a, g, parts, nsets);
-  else if (add) hipLaunchKernelGGL((gn_apply_kernel<T, true, false>), grid, block, 0, s, a, g, parts, nsets);
-  else if (silu) hipLaunchKernelGGL((gn_apply_kernel<T, false, true>), grid, block, 0, s, a, g, parts, nsets);
-  else hipLaunchKernelGGL((gn_apply_kernel<T, false, false>), grid, block, 0, s, a, g, parts, nsets);
+  if (add && silu) hipLaunchKernelGGL((gn_apply_kernel<T, true, true, FIN>), grid, block, 0, s, a, g, parts, nsets);
+  else if (add) hipLaunchKernelGGL((gn_apply_kernel<T, true, false, FIN>), grid, block, 0, s, a, g, parts, nsets);
+  else if (silu) hipLaunchKernelGGL((gn_apply_kernel<T, false, true, FIN>), grid, block, 0, s, a, g, parts, nsets);
+  else hipLaunchKernelGGL((gn_apply_kernel<T, false, false, FIN>), grid, block, 0, s, a, g, parts, nsets);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -727,6 +770,29 @@ extern "C" int vp2p_group_norm_apply(const vp2p_group_norm_args* a, const float*
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a->dtype == VP2P_BF16) gn_apply_launch<bf16>(*a, g, partials, nsets, s);
   else gn_apply_launch<float>(*a, g, partials, nsets, s);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_finalize(const vp2p_group_norm_args* a, const float* partials, int32_t nsets,
+                                        float* stats, void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!partials || !stats || nsets <= 0) return VP2P_E_ARG;
+  if ((int64_t)nsets * g.parts >= ((int64_t)1 << 31)) return VP2P_E_SHAPE;
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(a->groups, a->batch), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     *a, g, partials, nsets, stats);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_apply_stats(const vp2p_group_norm_args* a, const float* stats, void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!stats) return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a->dtype == VP2P_BF16) gn_apply_launch<bf16, true>(*a, g, stats, 1, s);
+  else gn_apply_launch<float, true>(*a, g, stats, 1, s);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 

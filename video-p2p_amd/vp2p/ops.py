@@ -383,6 +383,12 @@ def _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out):
                               rows, C, num_groups, float(eps), int(silu), dt)
 
 
+# Partial sets from which the finalize launch (~5 us) pays for itself: below it every apply block
+# merges the few partials itself (profiles/r02_gn_finalize_ab.jsonl: 8x8 latents, 22 partials:
+# 8.6 us merged in the apply vs 5.3 + 5.8; 64x64 at 320 channels, 249 partials: 44.0 vs 6.3 + 31.9).
+GN_FINALIZE_MIN_PARTS = 128
+
+
 def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
                eps: float, frames: int, silu: bool = False, add: Optional[torch.Tensor] = None,
                shard=None, out: Optional[torch.Tensor] = None, return_stats: bool = False):
@@ -408,7 +414,15 @@ def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor],
     if shard is not None and shard.world > 1:
         partials = shard.all_gather_flat(partials)
         nsets = shard.world
-    check(lib.vp2p_group_norm_apply(ctypes.byref(a), _ptr(partials), nsets, s), "vp2p_group_norm_apply")
+    if parts * nsets >= GN_FINALIZE_MIN_PARTS:
+        # one finalize launch merges the partials into (mean, rstd) per (batch, group); the apply
+        # blocks then read 2 floats per group instead of each merging every partial
+        st = torch.empty((Bf // frames) * num_groups * 2, device=x.device, dtype=torch.float32)
+        check(lib.vp2p_group_norm_finalize(ctypes.byref(a), _ptr(partials), nsets, _ptr(st), s),
+              "vp2p_group_norm_finalize")
+        check(lib.vp2p_group_norm_apply_stats(ctypes.byref(a), _ptr(st), s), "vp2p_group_norm_apply_stats")
+    else:
+        check(lib.vp2p_group_norm_apply(ctypes.byref(a), _ptr(partials), nsets, s), "vp2p_group_norm_apply")
     if return_stats:
         return out, (partials, nsets)
     return out
