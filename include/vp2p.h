@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 9
+#define VP2P_ABI_VERSION 10
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -255,6 +255,11 @@ typedef struct vp2p_group_norm_args {
   float eps;
   int32_t silu;             /* apply x * sigmoid(x) after the affine */
   int32_t dtype;
+  /* two-source input (the up blocks' torch.cat([hidden, skip], dim=1), unet_blocks.py: the cat is
+   * never written): x holds channels [0, channels - channels2) with that row stride, x2 the last
+   * channels2 (row stride channels2); both % 8 == 0.  NULL / 0: x holds all channels.  Forward only. */
+  const void* x2;
+  int32_t channels2;
 } vp2p_group_norm_args;
 
 int32_t vp2p_group_norm_parts(const vp2p_group_norm_args* args);   /* <0: unsupported shape */
@@ -335,6 +340,11 @@ typedef struct vp2p_conv_args {
   int32_t ksplit;           /* set by the library; callers leave 0 */
   int32_t upsample;         /* 1: x is (batch, in_h/2, in_w/2, cin), nearest-upsampled x2 on the fly
                                (Upsample3D's F.interpolate, resnet.py:79-99); stride 1 only */
+  /* two-source input of a 1x1 conv (the up blocks' resnet conv_shortcut on torch.cat([hidden, skip])):
+   * x holds input channels [0, cin - cin2) (row stride cin - cin2), x2 the last cin2 (row stride
+   * cin2); both % 64 == 0.  NULL / 0: x holds all cin channels. */
+  const void* x2;
+  int32_t cin2;
 } vp2p_conv_args;
 
 int vp2p_conv2d_supported(const vp2p_conv_args* args);

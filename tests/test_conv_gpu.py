@@ -78,6 +78,28 @@ def test_conv2d_splitk_residual():
     assert _lib.load().vp2p_conv2d_workspace_bytes(ctypes.byref(a)) > 0     # the split path ran
 
 
+@pytest.mark.parametrize("n,c1,c2,h,cout,residual", [(32, 320, 320, 16, 320, True), (4, 1280, 640, 8, 640, False),
+                                                      (2, 640, 1280, 8, 1280, True), (1, 2560, 1280, 4, 1280, False)])
+def test_conv2d_two_sources(n, c1, c2, h, cout, residual):
+    """conv_shortcut of an up-block resnet on torch.cat([hidden, skip], dim=1) read from the two
+    tensors: bit-equal to K10 on the materialised cat (same K-step order), incl. split-K shapes."""
+    from vp2p import ops
+    g = torch.Generator().manual_seed(11)
+    x1 = torch.randn(n, c1, h, h, generator=g).to(torch.bfloat16).to(DEV).to(memory_format=torch.channels_last)
+    x2 = torch.randn(n, c2, h, h, generator=g).to(torch.bfloat16).to(DEV).to(memory_format=torch.channels_last)
+    w = (torch.randn(cout, c1 + c2, 1, 1, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(cout, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    r = (torch.randn(n, cout, h, h, generator=g).to(torch.bfloat16).to(DEV).to(memory_format=torch.channels_last)
+         if residual else None)
+    cat = torch.cat([x1, x2], dim=1).contiguous(memory_format=torch.channels_last)
+    assert ops.conv2d_supported(x1, w, 1, 0, x2=x2)
+    ref = ops.conv2d(cat, w, b, 1, 0, residual=r)
+    out = ops.conv2d(x1, w, b, 1, 0, residual=r, x2=x2)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert not ops.conv2d_supported(x1, torch.randn(cout, c1 + c2, 3, 3, device=DEV, dtype=torch.bfloat16), 1, 1, x2=x2)
+
+
 def test_conv2d_unsupported_raises():
     from vp2p import ops, _lib
     x = torch.randn(1, 4, 8, 8, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)

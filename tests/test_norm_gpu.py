@@ -53,6 +53,30 @@ def test_group_norm(dtype, B, f, C, H, G, add, silu, offset):
     assert _rel(out.float(), ref) < TOL[dtype], _rel(out.float(), ref)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,f,C1,C2,H,add,silu", [
+    (2, 8, 320, 320, 16, True, True),       # up block res-64: cat(hidden 320, skip 320), 20 ch/group
+    (1, 8, 1280, 640, 8, False, True),      # cat(1280, 640) = 1920: groups of 60 straddle the seam
+    (2, 4, 640, 320, 8, True, False),       # 960: groups of 30
+    (1, 3, 1280, 1280, 16, True, True),     # large: the finalize + apply_stats path
+])
+def test_group_norm_two_sources(dtype, B, f, C1, C2, H, add, silu):
+    """norm1 of an up-block resnet reads torch.cat([hidden, skip], dim=1) from the two tensors: equal
+    bit for bit to the norm of the materialised cat (same per-column reads, same sums)."""
+    from vp2p import ops
+    x1 = _rand((B * f, C1, H, H), 5, dtype).cuda().to(memory_format=torch.channels_last)
+    x2 = _rand((B * f, C2, H, H), 6, dtype, 2.0, 0.5).cuda().to(memory_format=torch.channels_last)
+    C = C1 + C2
+    w, b = _rand((C,), 7, dtype, 0.3, 1.0).cuda(), _rand((C,), 8, dtype, 0.3).cuda()
+    t = _rand((B * f, C), 9, dtype, 0.7).cuda() if add else None
+    cat = torch.cat([x1, x2], dim=1).contiguous(memory_format=torch.channels_last)
+    ref = ops.group_norm(cat, 32, w, b, 1e-5, f, silu=silu, add=t)
+    out = ops.group_norm(x1, 32, w, b, 1e-5, f, silu=silu, add=t, x2=x2)
+    torch.cuda.synchronize()
+    assert out.shape == cat.shape and out.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(out, ref)
+
+
 def test_group_norm_partials_merge_across_sets():
     """The frame-sharded form: stats of each frame half computed separately, merged by apply."""
     from vp2p import ops, _lib

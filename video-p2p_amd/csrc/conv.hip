@@ -145,9 +145,10 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
   uint32_t a_off[G_ADMA], a_bad[G_ADMA], b_off[G_BDMA];
   __amdgpu_buffer_rsrc_t xr, wr;
   const int sh = a.in_h >> (AM == 2), sw = a.in_w >> (AM == 2);   // stored image
+  const int cin1 = a.cin - a.cin2;       // channels (and row stride) of x; x2 holds the last cin2
   if constexpr (AM != 0) {
     xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0,
-                                           (uint32_t)a.batch * sh * sw * a.cin * 2u, 0x00020000);
+                                           (uint32_t)a.batch * sh * sw * cin1 * 2u, 0x00020000);
     wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, (uint32_t)a.cout * Kw * 2u, 0x00020000);
 #pragma unroll
     for (int i = 0; i < G_ADMA; ++i) {
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
         const int oy = a_iy[i] + a.pad, ox = a_ix[i] + a.pad;       // stride 1
         a_off[i] = (uint32_t)((((a_n[i] * sh + (oy >> 1)) * sw + (ox >> 1)) * a.cin + a_c[i]) * 2);
       } else {
-        a_off[i] = (uint32_t)((((a_n[i] * a.in_h + a_iy[i]) * a.in_w + a_ix[i]) * a.cin + a_c[i]) * 2);
+        a_off[i] = (uint32_t)((((a_n[i] * a.in_h + a_iy[i]) * a.in_w + a_ix[i]) * cin1 + a_c[i]) * 2);
       }
       uint32_t bad = 0;
 #pragma unroll
@@ -175,6 +176,18 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
     }
   }
 
+  // two-source 1x1 input: the pixel's offsets in x2 (row stride cin2) for the K-steps past cin1
+  uint32_t a_off2[G_ADMA];
+  __amdgpu_buffer_rsrc_t xr2 = xr;
+  if constexpr (AM == 1 && KS == 1) {
+    if (a.x2) {
+      xr2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x2), 0,
+                                              (uint32_t)a.batch * a.in_h * a.in_w * a.cin2 * 2u, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < G_ADMA; ++i)
+        a_off2[i] = (uint32_t)((((a_n[i] * a.in_h + a_iy[i]) * a.in_w + a_ix[i]) * a.cin2 + a_c[i]) * 2);
+    }
+  }
   const int csteps = a.cin / BK;
   const int nall = KS * KS * csteps;
   const int s_begin = (int)((int64_t)nall * split / ks_n), s_end = (int)((int64_t)nall * (split + 1) / ks_n);
@@ -196,8 +209,14 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
                                                    16, o | ((a_bad[i] >> tap) << 31), 0, 0, 0);
         }
+      } else if (KS == 1 && a.x2 && c0 >= cin1) {           // 1x1, second source (wave-uniform)
+        const uint32_t xs = (uint32_t)((c0 - cin1) * 2);
+#pragma unroll
+        for (int i = 0; i < G_ADMA; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr2, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
+                                                   16, (a_off2[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
       } else {
-        const uint32_t xs = (uint32_t)(((kh * a.in_w + kw) * a.cin + c0) * 2);
+        const uint32_t xs = (uint32_t)(((kh * a.in_w + kw) * cin1 + c0) * 2);
 #pragma unroll
         for (int i = 0; i < G_ADMA; ++i)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
@@ -410,6 +429,12 @@ extern "C" int vp2p_conv2d_supported(const vp2p_conv_args* a) {
   if (a->epilogue != VP2P_CONV_EPI_NONE &&
       (a->epilogue != VP2P_CONV_EPI_GEGLU || a->kernel != 1 || a->stride != 1 || a->residual)) return 0;
   if (a->upsample != 0 && (a->upsample != 1 || a->stride != 1 || (a->in_h & 1) || (a->in_w & 1))) return 0;
+  if (a->x2 || a->cin2) {   // two-source input: 1x1 convs on the buffer-offset form only
+    if (!a->x2 || a->cin2 <= 0 || a->cin2 >= a->cin || a->cin2 % conv::BK || a->kernel != 1 || a->stride != 1 ||
+        a->upsample || a->epilogue != VP2P_CONV_EPI_NONE)
+      return 0;
+    if ((int64_t)a->batch * a->in_h * a->in_w * a->cin * 2 >= ((int64_t)1 << 31)) return 0;
+  }
   return 1;
 }
 
@@ -424,7 +449,7 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   if (a->dtype != VP2P_BF16) return VP2P_E_DTYPE;
   if (!vp2p_conv2d_supported(a)) return VP2P_E_SHAPE;
   for (const void* p : {a->x, a->w, static_cast<const void*>(a->y), a->residual,
-                        static_cast<const void*>(a->workspace)})
+                        static_cast<const void*>(a->workspace), a->x2})
     if (reinterpret_cast<uintptr_t>(p) & 15) return VP2P_E_ARG;
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   if (M * a->cout > ((int64_t)1 << 40)) return VP2P_E_SHAPE;

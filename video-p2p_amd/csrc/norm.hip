@@ -101,11 +101,25 @@ static bool gn_geom(const vp2p_group_norm_args* a, GnGeom* g) {
 
 constexpr int kUnroll = 4;
 
-// x (+ add of the row's sample) of one 8-channel vector, rounded to T like torch's h + temb
+// This thread's input column (8-channel vector v of batch element b) and its row stride: x, or x2
+// for the channels of a two-source input's second part
+template <typename T>
+__device__ __forceinline__ const T* gn_src(const vp2p_group_norm_args& a, const GnGeom& g, int b, int v, int& stride) {
+  const int c1 = a.channels - a.channels2;
+  if (a.x2 && v * 8 >= c1) {
+    stride = a.channels2;
+    return static_cast<const T*>(a.x2) + (int64_t)b * g.L * a.channels2 + (v * 8 - c1);
+  }
+  stride = c1;
+  return static_cast<const T*>(a.x) + (int64_t)b * g.L * c1 + v * 8;
+}
+
+// x (+ add of the row's sample) of one 8-channel vector, rounded to T like torch's h + temb;
+// x points at the thread's column, xs is its row stride
 template <typename T, bool ADD>
-__device__ __forceinline__ void load_row(const vp2p_group_norm_args& a, const T* x, int b, int64_t row, int v,
-                                         float (&val)[8]) {
-  V8<T>::load(x + row * a.channels, val);
+__device__ __forceinline__ void load_row(const vp2p_group_norm_args& a, const T* x, int xs, int b, int64_t row,
+                                         int v, float (&val)[8]) {
+  V8<T>::load(x + row * xs, val);
   if (ADD) {
     float ad[8];
     const int fr = (int)((uint32_t)row / (uint32_t)a.rows);     // L = frames * rows < 2^31 (gn_geom)
@@ -127,18 +141,19 @@ __global__ __launch_bounds__(512) void gn_stats_kernel(const vp2p_group_norm_arg
   const int v = tid % nvec, r = tid / nvec;
   const int64_t row0 = (int64_t)part * g.chunk;
   const int64_t row1 = row0 + g.chunk < g.L ? row0 + g.chunk : g.L;
-  const T* x = static_cast<const T*>(a.x) + (int64_t)b * g.L * C + v * 8;
+  int xs;
+  const T* x = gn_src<T>(a, g, b, v, xs);
   float K[8], s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { K[j] = 0.f; s1[j] = 0.f; s2[j] = 0.f; }
   int n = 0;
   int64_t row = row0 + r;
-  if (row < row1) load_row<T, ADD>(a, x, b, row, v, K);     // shift: the thread's first value
+  if (row < row1) load_row<T, ADD>(a, x, xs, b, row, v, K);     // shift: the thread's first value
   // kUnroll rows in flight per thread: all loads issued before any is consumed
   for (; row + (kUnroll - 1) * R < row1; row += kUnroll * R) {
     float val[kUnroll][8];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) load_row<T, ADD>(a, x, b, row + u * R, v, val[u]);
+    for (int u = 0; u < kUnroll; ++u) load_row<T, ADD>(a, x, xs, b, row + u * R, v, val[u]);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
@@ -151,7 +166,7 @@ __global__ __launch_bounds__(512) void gn_stats_kernel(const vp2p_group_norm_arg
   }
   for (; row < row1; row += R) {
     float val[8];
-    load_row<T, ADD>(a, x, b, row, v, val);
+    load_row<T, ADD>(a, x, xs, b, row, v, val);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float d = val[j] - K[j];
@@ -282,7 +297,8 @@ __global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_arg
   const int64_t row0 = (int64_t)part * g.chunk;
   const int64_t row1 = row0 + g.chunk < g.L ? row0 + g.chunk : g.L;
   const int64_t base = (int64_t)b * g.L * C + v * 8;
-  const T* x = static_cast<const T*>(a.x) + base;
+  int xs;
+  const T* x = gn_src<T>(a, g, b, v, xs);
   T* y = static_cast<T*>(a.y) + base;
   auto finish = [&](float (&val)[8]) {
 #pragma unroll
@@ -296,7 +312,7 @@ __global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_arg
   for (; row + (kUnroll - 1) * R < row1; row += kUnroll * R) {
     float val[kUnroll][8];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) load_row<T, ADD>(a, x, b, row + u * R, v, val[u]);
+    for (int u = 0; u < kUnroll; ++u) load_row<T, ADD>(a, x, xs, b, row + u * R, v, val[u]);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       finish(val[u]);
@@ -305,7 +321,7 @@ __global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_arg
   }
   for (; row < row1; row += R) {
     float val[8];
-    load_row<T, ADD>(a, x, b, row, v, val);
+    load_row<T, ADD>(a, x, xs, b, row, v, val);
     finish(val);
     V8<T>::store(y + row * C, val);
   }
@@ -313,6 +329,8 @@ __global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_arg
 
 static int gn_check(const vp2p_group_norm_args* a, GnGeom* g) {
   if (!a || !a->x || !a->y) return VP2P_E_ARG;
+  if (a->x2 ? (a->channels2 <= 0 || a->channels2 >= a->channels || a->channels2 % 8) : a->channels2 != 0)
+    return VP2P_E_ARG;
   if (a->dtype != VP2P_F32 && a->dtype != VP2P_BF16) return VP2P_E_DTYPE;
   if (!gn_geom(a, g)) return VP2P_E_SHAPE;
   return VP2P_OK;
@@ -537,9 +555,10 @@ __global__ __launch_bounds__(512) void gn_bwd_reduce_kernel(const vp2p_group_nor
   const int64_t row1 = row0 + g.chunk < g.L ? row0 + g.chunk : g.L;
   const int64_t base = (int64_t)b * g.L * C + v * 8;
   const T* x = static_cast<const T*>(a.x) + base;
+  const int xs = C;
   for (int64_t row = row0 + r; row < row1; row += R) {
     float xv[8], dv[8];
-    load_row<T, ADD>(a, x, b, row, v, xv);
+    load_row<T, ADD>(a, x, xs, b, row, v, xv);
     V8<T>::load(dy + base + row * C, dv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -634,9 +653,10 @@ __global__ __launch_bounds__(512) void gn_bwd_apply_kernel(const vp2p_group_norm
   const int64_t row1 = row0 + g.chunk < g.L ? row0 + g.chunk : g.L;
   const int64_t base = (int64_t)b * g.L * C + v * 8;
   const T* x = static_cast<const T*>(a.x) + base;
+  const int xs = C;
   for (int64_t row = row0 + r; row < row1; row += R) {
     float xv[8], dv[8];
-    load_row<T, ADD>(a, x, b, row, v, xv);
+    load_row<T, ADD>(a, x, xs, b, row, v, xv);
     V8<T>::load(dy + base + row * C, dv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -871,6 +891,7 @@ extern "C" int vp2p_group_norm_bwd_reduce(const vp2p_group_norm_args* a, const f
   GnGeom g;
   int rc = gn_check(a, &g);
   if (rc != VP2P_OK) return rc;
+  if (a->x2) return VP2P_E_ARG;                       // forward only
   if (!partials || nsets <= 0 || !dy || !bwd_partials) return VP2P_E_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid(g.parts, a->batch), block(g.threads);
@@ -895,6 +916,7 @@ extern "C" int vp2p_group_norm_bwd_apply(const vp2p_group_norm_args* a, const fl
   GnGeom g;
   int rc = gn_check(a, &g);
   if (rc != VP2P_OK) return rc;
+  if (a->x2) return VP2P_E_ARG;                       // forward only
   if (!partials || nsets <= 0 || !dy || !bwd_partials || bsets <= 0 || !dx) return VP2P_E_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid(g.parts, a->batch), block(g.threads);

@@ -366,9 +366,14 @@ def _rows_view(x: torch.Tensor) -> torch.Tensor:
     return x.reshape(-1, x.shape[-1])
 
 
-def _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out):
-    Bf, C = x.shape[0], x.shape[1]
+def _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out, x2=None):
+    Bf, C = x.shape[0], x.shape[1] + (0 if x2 is None else x2.shape[1])
     xm = _rows_view(x)
+    x2m = None
+    if x2 is not None:
+        x2m = _rows_view(x2)
+        if x2.dtype != x.dtype or x2.shape[0] != Bf or x2.shape[2:] != x.shape[2:]:
+            raise ValueError("x2 must match x in dtype, samples and spatial size")
     dt = _dtype(xm)
     if Bf % frames:
         raise ValueError(f"{Bf} samples are not a multiple of {frames} frames")
@@ -379,8 +384,11 @@ def _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out):
             raise ValueError("weight/bias/add must be contiguous device tensors of the activation dtype")
     if add is not None and tuple(add.shape) != (Bf, C):
         raise ValueError(f"add must be (Bf, C) = {(Bf, C)}, got {tuple(add.shape)}")
-    return _lib.GroupNormArgs(_ptr(xm), _ptr(add), _ptr(ym), _ptr(weight), _ptr(bias), None, Bf // frames, frames,
-                              rows, C, num_groups, float(eps), int(silu), dt)
+    a = _lib.GroupNormArgs(_ptr(xm), _ptr(add), _ptr(ym), _ptr(weight), _ptr(bias), None, Bf // frames, frames,
+                           rows, C, num_groups, float(eps), int(silu), dt)
+    if x2 is not None:
+        a.x2, a.channels2 = _ptr(x2m), x2.shape[1]
+    return a
 
 
 # Partial sets from which the finalize launch (~5 us) pays for itself: below it every apply block
@@ -391,17 +399,23 @@ GN_FINALIZE_MIN_PARTS = 128
 
 def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
                eps: float, frames: int, silu: bool = False, add: Optional[torch.Tensor] = None,
-               shard=None, out: Optional[torch.Tensor] = None, return_stats: bool = False):
+               shard=None, out: Optional[torch.Tensor] = None, return_stats: bool = False,
+               x2: Optional[torch.Tensor] = None):
     """GroupNorm of a ``(b f) c h w`` channels-last tensor with statistics over (c/G, f, h, w) of
     each batch element (tuneavideo resnet.py:142,158; frames=1: per-frame, attention.py:110),
     optionally on x + add[(b f), c] (the resnet's h + temb, resnet.py:149-156) and followed by SiLU.
     ``shard``: a FrameShard whose ranks hold the other frames; their partial statistics are
     gathered between the two kernels.  ``return_stats``: also return (partials, nsets), the
-    statistics the backward needs."""
+    statistics the backward needs.  ``x2``: normalise torch.cat([x, x2], dim=1) (channels-last,
+    forward only) without writing the cat."""
     Bf = x.shape[0]
     if out is None:
-        out = torch.empty_like(x)
-    a = _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out)
+        if x2 is None:
+            out = torch.empty_like(x)
+        else:
+            out = torch.empty((Bf, x.shape[1] + x2.shape[1]) + tuple(x.shape[2:]), device=x.device, dtype=x.dtype,
+                              memory_format=torch.channels_last)
+    a = _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out, x2)
     lib = _lib.load()
     parts = lib.vp2p_group_norm_parts(ctypes.byref(a))
     if parts < 0:
@@ -523,8 +537,10 @@ def geglu_bwd(h: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
 
 
 def _conv_args(x: torch.Tensor, weight: torch.Tensor, bias, residual, y, stride: int, padding: int,
-               upsample: bool = False):
+               upsample: bool = False, x2: Optional[torch.Tensor] = None):
     N, Cin, H, W = x.shape
+    if x2 is not None:
+        Cin += x2.shape[1]
     if upsample:
         H, W = 2 * H, 2 * W
     Cout, _, KH, KW = weight.shape
@@ -534,11 +550,13 @@ def _conv_args(x: torch.Tensor, weight: torch.Tensor, bias, residual, y, stride:
     a = _lib.ConvArgs(_ptr(x), _ptr(weight), _ptr(bias), _ptr(residual), _ptr(y), N, H, W, Cin, Cout, Ho, Wo,
                       KH if KH == KW else -1, stride, padding, dt)
     a.upsample = 1 if upsample else 0
+    if x2 is not None:
+        a.x2, a.cin2 = _ptr(x2), x2.shape[1]
     return a, (N, Cout, Ho, Wo)
 
 
 def conv2d_supported(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0,
-                     upsample: bool = False) -> bool:
+                     upsample: bool = False, x2: Optional[torch.Tensor] = None) -> bool:
     """True when K10 covers this convolution: bf16, channels-last, 1x1 / 3x3 'same' padding, stride
     1 or 2, Cin % 64 == 0, Cout % 160 == 0 (every resnet / up/down-sample conv of the SD-1.5 UNet
     except conv_in / conv_out)."""
@@ -546,12 +564,16 @@ def conv2d_supported(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad
         return False
     if not x.is_contiguous(memory_format=torch.channels_last):
         return False
-    a, _ = _conv_args(x, weight, None, None, None, stride, padding, upsample)
+    if x2 is not None and (x2.dtype != x.dtype or x2.shape[0] != x.shape[0] or x2.shape[2:] != x.shape[2:]
+                           or not x2.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    a, _ = _conv_args(x, weight, None, None, None, stride, padding, upsample, x2)
     return bool(_lib.load().vp2p_conv2d_supported(ctypes.byref(a)))
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
-           padding: int = 0, residual: Optional[torch.Tensor] = None, upsample: bool = False) -> torch.Tensor:
+           padding: int = 0, residual: Optional[torch.Tensor] = None, upsample: bool = False,
+           x2: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K10: nn.Conv2d on channels-last bf16 with the bias and an optional residual add fused
     (``residual + conv(x)``, the resnet shortcut add of resnet.py:196-205).  Returns a channels-last
     (N, Cout, Ho, Wo) tensor.  Raises for shapes K10 does not cover (see ``conv2d_supported``)."""
@@ -561,7 +583,9 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
         weight.contiguous(memory_format=torch.channels_last)
     if bias is not None and (bias.dtype != x.dtype or not bias.is_contiguous()):
         bias = bias.to(x.dtype).contiguous()
-    a, shape = _conv_args(x, w, bias, None, None, stride, padding, upsample)
+    if x2 is not None and not x2.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv2d: x2 must be channels-last contiguous")
+    a, shape = _conv_args(x, w, bias, None, None, stride, padding, upsample, x2)
     y = torch.empty(shape, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
     if residual is not None:
         if residual.shape != y.shape or residual.dtype != y.dtype:
@@ -621,16 +645,20 @@ class ConvSelector:
             self.choice[ks] = use
         return use
 
-    def run(self, x, weight, bias, stride: int, padding: int, residual, library, upsample: bool = False):
+    def run(self, x, weight, bias, stride: int, padding: int, residual, library, upsample: bool = False,
+            x2: Optional[torch.Tensor] = None):
+        """``x2``: the input is torch.cat([x, x2], dim=1); K10 reads the two parts (1x1), ``library``
+        must build the cat itself.  The table key is the cat's shape."""
         def k10():
-            return conv2d(x, weight, bias, stride, padding, residual=residual, upsample=upsample)
+            return conv2d(x, weight, bias, stride, padding, residual=residual, upsample=upsample, x2=x2)
 
         def lib():
             y = library()
             return y if residual is None else residual + y
 
-        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, residual is not None, upsample)
-        if self.pick(key, conv2d_supported(x, weight, stride, padding, upsample), k10, lib):
+        xs = tuple(x.shape) if x2 is None else (x.shape[0], x.shape[1] + x2.shape[1]) + tuple(x.shape[2:])
+        key = ("conv", xs, tuple(weight.shape), stride, padding, residual is not None, upsample)
+        if self.pick(key, conv2d_supported(x, weight, stride, padding, upsample, x2), k10, lib):
             return k10()
         return lib()
 

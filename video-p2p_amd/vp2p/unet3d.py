@@ -39,12 +39,18 @@ class UNet3DConditionOutput:
 
 
 def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bool = False,
-                      add: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      add: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None) -> torch.Tensor:
     """GroupNorm whose statistics span ``frames`` consecutive samples of a ``(b f) c h w``
     channels-last tensor (frames=1: the per-frame GroupNorm of Transformer3DModel.norm), applied
-    to ``x + add[:, :, None, None]`` when ``add`` ((b f), c) is given, then optionally SiLU (K7)."""
+    to ``x + add[:, :, None, None]`` when ``add`` ((b f), c) is given, then optionally SiLU (K7).
+    ``x2``: the input is torch.cat([x, x2], dim=1) (an up block's skip concatenation), read from the
+    two tensors without materialising the cat."""
+    if x2 is not None and autograd.needs_grad(x, x2, norm.weight, norm.bias, add):
+        x, x2 = torch.cat([x, x2], dim=1), None
     if not x.is_contiguous(memory_format=torch.channels_last):
         x = x.contiguous(memory_format=torch.channels_last)
+    if x2 is not None and not x2.is_contiguous(memory_format=torch.channels_last):
+        x2 = x2.contiguous(memory_format=torch.channels_last)
     shard = frame_parallel.active() if frames > 1 else None
     w, b = (norm.weight, norm.bias) if norm.affine else (None, None)
     add = None if add is None else add.contiguous()
@@ -52,7 +58,7 @@ def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bo
         if shard is not None and shard.world > 1:
             raise NotImplementedError("backward through a frame-sharded GroupNorm (run null-text clip-parallel)")
         return autograd.GroupNormFn.apply(x, add, w, b, norm.num_groups, norm.eps, frames, silu)
-    return ops.group_norm(x, norm.num_groups, w, b, norm.eps, frames, silu=silu, add=add, shard=shard)
+    return ops.group_norm(x, norm.num_groups, w, b, norm.eps, frames, silu=silu, add=add, shard=shard, x2=x2)
 
 
 def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
@@ -113,12 +119,16 @@ class InflatedConv3d(nn.Conv2d):
     MI355X, so every run and every rank takes the same numerics).  ``residual``: added to the output (the resnet
     shortcut add, fused on K10)."""
 
-    def forward(self, x, residual: Optional[torch.Tensor] = None):
+    def forward(self, x, residual: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None):
+        """``x2``: the input is torch.cat([x, x2], dim=1) (1x1 convs read the two parts on K10)."""
+        if x2 is not None and autograd.needs_grad(x, x2, self.weight, residual):
+            x, x2 = torch.cat([x, x2], dim=1), None
         if autograd.needs_grad(x, self.weight, residual):
             y = super().forward(x)
             return y if residual is None else residual + y
         return ops.CONV.run(x, self.weight, self.bias, self.stride[0], self.padding[0], residual,
-                            lambda: super(InflatedConv3d, self).forward(x))
+                            lambda: super(InflatedConv3d, self).forward(x if x2 is None else torch.cat([x, x2], 1)),
+                            x2=x2)
 
 
 class ResnetBlock3D(nn.Module):
@@ -135,12 +145,16 @@ class ResnetBlock3D(nn.Module):
         self.conv_shortcut = (InflatedConv3d(in_channels, out_channels, 1, 1, 0)
                               if in_channels != out_channels else None)
 
-    def forward(self, x, temb, frames):
-        h = self.conv1(group_norm_frames(x, self.norm1, frames, silu=True))
+    def forward(self, x, temb, frames, skip: Optional[torch.Tensor] = None):
+        """``skip``: the up blocks' input torch.cat([x, skip], dim=1) (unet_blocks.py CrossAttnUpBlock3D /
+        UpBlock3D), read by norm1 and conv_shortcut from the two tensors (the cat is never written)."""
+        if skip is not None and self.conv_shortcut is None:
+            x, skip = torch.cat([x, skip], dim=1), None
+        h = self.conv1(group_norm_frames(x, self.norm1, frames, silu=True, x2=skip))
         pre = self.__dict__.get("_temb_pre")      # this block's slice of UNet3D's batched projection
         t = pre if pre is not None else self.time_emb_proj(F.silu(temb))
         t = t.repeat_interleave(frames, 0).to(h.dtype)
-        sc = x if self.conv_shortcut is None else self.conv_shortcut(x)
+        sc = x if self.conv_shortcut is None else self.conv_shortcut(x, x2=skip)
         h = self.dropout(group_norm_frames(h, self.norm2, frames, silu=True, add=t))
         if self.output_scale_factor != 1.0:
             return (sc + self.conv2(h)) / self.output_scale_factor
@@ -349,8 +363,7 @@ class _UpBlock(nn.Module):
 
     def forward(self, x, skips, temb, ctx, frames, upsample_size=None):
         for i, r in enumerate(self.resnets):
-            x = torch.cat([x, skips[-1 - i]], dim=1)
-            x = r(x, temb, frames)
+            x = r(x, temb, frames, skip=skips[-1 - i])           # cat([x, skip], dim=1), not materialised
             if self.attentions is not None:
                 x = self.attentions[i](x, ctx, frames)
         if self.upsamplers is not None:
