@@ -181,8 +181,11 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
                           None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))
             return to_out(autograd.SharedKVAttention.apply(q, kv, f, h, module.scale))
         q = F.linear(x, module.to_q.weight, module.to_q.bias)
-        k = F.linear(ctx, module.to_k.weight, module.to_k.bias).contiguous()
-        v = F.linear(ctx, module.to_v.weight, module.to_v.bias).contiguous()
+        # K and V of the (B, 77, Cctx) context in one GEMM against [Wk; Wv]; K2's prep reads the views
+        kv = F.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
+                      None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))
+        Ck = module.to_k.weight.shape[0]
+        k, v = kv[..., :Ck], kv[..., Ck:]
         call = controller.fused_begin(True, place, N, f) if (controller is not None and fused) else LayerCall()
         call.cond_only = cond_only
         probs = None
@@ -198,7 +201,7 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
                                       probs_out=probs, prompts=P, scale=module.scale, cond_only=cond_only)
         if not fused:
             attn = controller(probs, True, place)
-            out = _pv(module, attn, v, B, f)
+            out = _pv(module, attn, v.contiguous(), B, f)
         elif controller is not None:
             controller.fused_end(True, place, call, probs)
         return to_out(out)

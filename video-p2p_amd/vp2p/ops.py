@@ -36,7 +36,8 @@ def _dtype(*ts):
 
 
 def _stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """The current HIP stream of the current device (the raw handle: no Stream object per launch)."""
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice()))
 
 
 def _ptr(t: Optional[torch.Tensor]):

@@ -126,9 +126,49 @@ class InflatedConv3d(nn.Conv2d):
         if autograd.needs_grad(x, self.weight, residual):
             y = super().forward(x)
             return y if residual is None else residual + y
+        if x2 is None and residual is None and self._padded_k10_fits(x):
+            return self._padded_k10(x)
         return ops.CONV.run(x, self.weight, self.bias, self.stride[0], self.padding[0], residual,
                             lambda: super(InflatedConv3d, self).forward(x if x2 is None else torch.cat([x, x2], 1)),
                             x2=x2)
+
+
+    def _padded_k10_fits(self, x) -> bool:
+        """conv_in (4 -> 320) and conv_out (320 -> 4): 3x3 'same' bf16 convs whose channel counts
+        miss K10's granularity (cin % 64, cout % 160)."""
+        cout, cin = self.weight.shape[:2]
+        return (x.dtype == torch.bfloat16 and x.is_cuda and self.kernel_size == (3, 3) and self.stride == (1, 1)
+                and self.padding == (1, 1) and self.groups == 1 and (cin % 64 or cout % 160)
+                and x.is_contiguous(memory_format=torch.channels_last))
+
+    def _padded_k10(self, x):
+        """K10 on channel-padded operands: zero input channels up to a multiple of 64, zero weight
+        rows up to a multiple of 160 (then the first cout output channels).  Keeps the library conv
+        (MIOpen, host-side solution lookup per call) off the UNet path; the zero padding adds
+        nothing to the sums."""
+        cout, cin = self.weight.shape[:2]
+        cin_p, cout_p = -(-cin // 64) * 64, -(-cout // 160) * 160
+        key = (self.weight.data_ptr(), self.weight._version, None if self.bias is None else self.bias._version)
+        cached = self.__dict__.get("_k10_pad")
+        if cached is None or cached[0] != key:
+            wp = self.weight.new_zeros((cout_p, cin_p, 3, 3))
+            wp[:cout, :cin] = self.weight.detach()
+            wp = wp.contiguous(memory_format=torch.channels_last)
+            bp = None
+            if self.bias is not None:
+                bp = self.bias.new_zeros(cout_p)
+                bp[:cout] = self.bias.detach()
+            cached = (key, wp, bp)
+            self.__dict__["_k10_pad"] = cached
+        _, wp, bp = cached
+        if cin_p != cin:
+            xp = torch.empty((x.shape[0], cin_p) + tuple(x.shape[2:]), device=x.device, dtype=x.dtype,
+                             memory_format=torch.channels_last)
+            xp[:, cin:].zero_()
+            xp[:, :cin] = x
+            x = xp
+        y = ops.conv2d(x, wp, bp, 1, 1)
+        return y if cout_p == cout else y[:, :cout]
 
 
 class ResnetBlock3D(nn.Module):
