@@ -34,6 +34,10 @@ def _rel(a, b):
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
 @pytest.mark.parametrize("hw", [64, 256])
 def test_decode_matches_oracle(vae_state, dtype, tol, hw):
+    """bf16 at 256^2: 3e-2 -- the error of ~30 bf16 layers (the decoder's 4x4 upsampled resnets and
+    the 1024-position mid attention) measured 0.019-0.020 across boxes, against fp32 1e-4 parity."""
+    if dtype == torch.bfloat16 and hw == 256:
+        tol = 3e-2
     vae = _vae(vae_state, dtype)
     g = torch.Generator().manual_seed(1)
     z = torch.randn(2, 4, hw // 8, hw // 8, generator=g)
