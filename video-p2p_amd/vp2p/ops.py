@@ -398,6 +398,20 @@ def _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out, x2=None):
 GN_FINALIZE_MIN_PARTS = 128
 
 
+_GN_PARTS = {}      # (samples, frames, rows, channels, groups) -> partial sets of the stats launch
+
+
+def _gn_parts(lib, a) -> int:
+    key = (a.batch, a.frames, a.rows, a.channels, a.groups)
+    parts = _GN_PARTS.get(key)
+    if parts is None:
+        parts = lib.vp2p_group_norm_parts(ctypes.byref(a))
+        if parts < 0:
+            check(parts, "vp2p_group_norm_parts")
+        _GN_PARTS[key] = parts
+    return parts
+
+
 def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
                eps: float, frames: int, silu: bool = False, add: Optional[torch.Tensor] = None,
                shard=None, out: Optional[torch.Tensor] = None, return_stats: bool = False,
@@ -418,9 +432,7 @@ def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor],
                               memory_format=torch.channels_last)
     a = _gn_args(x, num_groups, weight, bias, eps, frames, silu, add, out, x2)
     lib = _lib.load()
-    parts = lib.vp2p_group_norm_parts(ctypes.byref(a))
-    if parts < 0:
-        check(parts, "vp2p_group_norm_parts")
+    parts = _gn_parts(lib, a)
     partials = torch.empty((Bf // frames) * parts * num_groups * 3, device=x.device, dtype=torch.float32)
     a.partials = partials.data_ptr()
     s = _stream()
@@ -572,6 +584,9 @@ def conv2d_supported(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad
     return bool(_lib.load().vp2p_conv2d_supported(ctypes.byref(a)))
 
 
+_CONV_WS = {}       # conv geometry -> split-K workspace bytes (a pure function of the shape)
+
+
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
            padding: int = 0, residual: Optional[torch.Tensor] = None, upsample: bool = False,
            x2: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -596,7 +611,10 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
         a.residual = _ptr(residual)
     a.y = _ptr(y)
     lib = _lib.load()
-    wsb = lib.vp2p_conv2d_workspace_bytes(ctypes.byref(a))
+    wkey = (a.batch, a.in_h, a.in_w, a.cin, a.cout, a.kernel, a.stride, a.pad, a.upsample, a.cin2, a.epilogue)
+    wsb = _CONV_WS.get(wkey)
+    if wsb is None:
+        wsb = _CONV_WS[wkey] = lib.vp2p_conv2d_workspace_bytes(ctypes.byref(a))
     ws = None
     if wsb > 0:      # split-K slices (small-M shapes); from the caching allocator, no sync
         ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
@@ -629,6 +647,7 @@ class ConvSelector:
             with open(self.TABLE) as fh:
                 self.table = {k: bool(v) for k, v in json.load(fh)["choices"].items()}
         self.choice = {}
+        self._supported = {}
 
     @staticmethod
     def key_str(key) -> str:
@@ -659,7 +678,12 @@ class ConvSelector:
 
         xs = tuple(x.shape) if x2 is None else (x.shape[0], x.shape[1] + x2.shape[1]) + tuple(x.shape[2:])
         key = ("conv", xs, tuple(weight.shape), stride, padding, residual is not None, upsample)
-        if self.pick(key, conv2d_supported(x, weight, stride, padding, upsample, x2), k10, lib):
+        skey = (key, x2 is not None, x.dtype, weight.dtype, x.is_cuda, x.is_contiguous(memory_format=torch.channels_last),
+                x2 is None or x2.is_contiguous(memory_format=torch.channels_last))
+        sup = self._supported.get(skey)
+        if sup is None:       # a pure function of shapes, dtypes and layouts: asked once per key
+            sup = self._supported[skey] = conv2d_supported(x, weight, stride, padding, upsample, x2)
+        if self.pick(key, sup, k10, lib):
             return k10()
         return lib()
 
