@@ -97,7 +97,7 @@ __global__ void cross_kv_prep_kernel(const T* __restrict__ k, const T* __restric
 // LocalBlend head sum is finished by cross_lb_reduce_kernel from per-head partials, in head order.
 template <typename T, int D, int KB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CrossCfg<T, D>::OCC, 8)))
-void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
+void cross_attn_kernel(const vp2p_cross_attn_args a, int prow, int g0) {
   using M = Mfma<T>;
   using C = CrossCfg<T, D>;
   constexpr int KP = 32 * KB;
@@ -110,7 +110,7 @@ void cross_attn_kernel(const vp2p_cross_attn_args a, int prow) {
   const int items = qblocks * hgroups;
   const bool p2p = a.prompts > 0 && a.batch == (a.cond_only ? 1 : 2) * a.prompts;
   const int RP = p2p ? a.prompts : 1;          // rows per group
-  const int g = blockIdx.y;                    // group: CFG half (p2p) or batch row
+  const int g = g0 + (int)blockIdx.y;          // group: CFG half (p2p) or batch row
   const bool cond = p2p && (a.cond_only || g == 1);   // cond_only: the one group is the conditional half
   const bool edit = cond && (a.edit_mode != VP2P_EDIT_NONE || a.reweight);
   const bool lb = cond && a.lb_acc != nullptr;
@@ -350,7 +350,7 @@ struct CrossV3Cfg {
 };
 
 template <int D, int KB>
-__global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(const vp2p_cross_attn_args a, int iters) {
+__global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(const vp2p_cross_attn_args a, int iters, int b0) {
   using T = bf16;
   using M = Mfma<T>;
   using C = CrossCfg<T, D>;
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int FQ = a.frames * a.tokens_q;
   const bool p2p = a.prompts > 0 && a.batch == (a.cond_only ? 1 : 2) * a.prompts;
-  const int b = blockIdx.y;                     // batch row
+  const int b = b0 + (int)blockIdx.y;          // batch row
   const int head = blockIdx.z;
   const int g = p2p ? b / a.prompts : 0;        // CFG half
   const int pw = p2p ? b - g * a.prompts : 0;   // prompt within the half
@@ -572,27 +572,40 @@ static int cross_nonedit_kernel() {
 template <typename T, int D, int KB>
 static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
   const int FQ = a->frames * a->tokens_q;
+  // v3 over batch rows [b0, b0 + rows): every row of a non-edit launch, or the unconditional half of
+  // an edit launch (the reference edits only attn[h//2:], run_videop2p.py:217-218)
+  auto launch_v3 = [&](int b0, int rows) -> int {
+    using V3 = CrossV3Cfg<D, KB>;
+    const int64_t qblocks = (FQ + 31) / 32;
+    const int64_t per_wg = (qblocks + 3) / 4;                   // iterations of one stream, all blocks
+    const int64_t gh = (int64_t)rows * a->heads;
+    // ~4 workgroups per CU over the (row, head) grid; each stream then loops `iters` blocks
+    int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (1024 + gh - 1) / gh));
+    const int iters = (int)((per_wg + nx - 1) / nx);
+    nx = (per_wg + iters - 1) / iters;
+    if (rows > 65535 || a->heads > 65535 || nx > 0x7fffffff) return VP2P_E_SHAPE;
+    const int sets = a->lb_sets == 2 ? 2 : 1;
+    const size_t lds = (size_t)V3::LDS + (size_t)sets * a->tokens_kv * sizeof(float);
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    if (!attr || lds > 160 * 1024) return VP2P_E_LAUNCH;
+    hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB>), dim3((unsigned)nx, (unsigned)rows, (unsigned)a->heads),
+                       dim3(256), lds, s, *a, iters, b0);
+    return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+  };
+  int g_first = 0;              // first CFG half / batch row the v1 kernel takes
   if constexpr (sizeof(T) == 2) {
     const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
     const bool edit = p2p && (a->edit_mode != VP2P_EDIT_NONE || a->reweight);
+    if (edit && !a->cond_only && cross_nonedit_kernel() == 3) {
+      const int rc = launch_v3(0, a->prompts);     // the unconditional half: plain attention on v3
+      if (rc != VP2P_OK) return rc;
+      g_first = 1;
+    }
     if (!edit && cross_nonedit_kernel() == 3) {
-      using V3 = CrossV3Cfg<D, KB>;
-      const int64_t qblocks = (FQ + 31) / 32;
-      const int64_t per_wg = (qblocks + 3) / 4;                 // iterations of one stream, all blocks
-      const int64_t gh = (int64_t)a->batch * a->heads;
-      // ~4 workgroups per CU over the (row, head) grid; each stream then loops `iters` blocks
-      int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (1024 + gh - 1) / gh));
-      const int iters = (int)((per_wg + nx - 1) / nx);
-      nx = (per_wg + iters - 1) / iters;
-      if (a->batch > 65535 || a->heads > 65535 || nx > 0x7fffffff) return VP2P_E_SHAPE;
+      const int rc = launch_v3(0, a->batch);
+      if (rc != VP2P_OK) return rc;
       const int sets = a->lb_sets == 2 ? 2 : 1;
-      const size_t lds = (size_t)V3::LDS + (size_t)sets * a->tokens_kv * sizeof(float);
-      static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB>),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-      if (!attr || lds > 160 * 1024) return VP2P_E_LAUNCH;
-      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB>), dim3((unsigned)nx, (unsigned)a->batch, (unsigned)a->heads),
-                         dim3(256), lds, s, *a, iters);
-      if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
       if (p2p && a->lb_acc) {
         const int64_t n = (int64_t)sets * a->prompts * FQ;
         const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
@@ -604,7 +617,7 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
     }
   }
   const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
-  const int groups = p2p ? (a->cond_only ? 1 : 2) : a->batch;
+  const int groups = (p2p ? (a->cond_only ? 1 : 2) : a->batch) - g_first;
   const int64_t items = (int64_t)((FQ + 31) / 32) * ((a->heads + 3) / 4);
   if (items <= 0 || groups > 65535) return VP2P_E_SHAPE;
   // One item per workgroup: measured faster at the UNet's shapes than a resident grid looping over
@@ -617,7 +630,7 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
   const size_t lds = (size_t)4 * 32 * prow * sizeof(float) + (size_t)(rp - 1) * a->tokens_kv * 16 +
                      (size_t)sets * rp * a->tokens_kv * sizeof(float);
   hipLaunchKernelGGL((cross_attn_kernel<T, D, KB>), dim3((unsigned)nwg, (unsigned)groups), dim3(256), lds, s,
-                     *a, prow);
+                     *a, prow, g_first);
   if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
   if (p2p && a->lb_acc) {   // (set, prompt) pairs are contiguous: reduce them as sets*prompts rows
     const int64_t n = (int64_t)sets * a->prompts * FQ;
