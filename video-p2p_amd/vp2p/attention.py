@@ -180,7 +180,7 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
             kv = F.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
                           None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))
             return to_out(autograd.SharedKVAttention.apply(q, kv, f, h, module.scale))
-        q = F.linear(x, module.to_q.weight, module.to_q.bias)
+        q = ops.linear(x, module.to_q.weight, module.to_q.bias)
         # K and V of the (B, 77, Cctx) context in one GEMM against [Wk; Wv]; K2's prep reads the views
         kv = F.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
                       None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))

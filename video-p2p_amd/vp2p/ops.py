@@ -14,6 +14,7 @@ import os
 from typing import Optional
 
 import torch
+import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check
@@ -759,6 +760,24 @@ def linear_residual(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.
         a.workspace = _ptr(ws)
     check(lib.vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd(linear)")
     return y
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x @ W^T + b (nn.Linear).  The K = 320 projections of the 64x64 latents (M >= 64k rows, N <= 640:
+    attn2's to_q and Transformer3DModel.proj_in at res-64) run on K10's GEMM core, measured faster than
+    hipBLASLt there (profiles/r02_linear_plain_ab.jsonl); every other shape, and anything that needs
+    a gradient, stays on hipBLASLt (F.linear).  A fixed shape rule: the same kernel every run."""
+    K, N = x.shape[-1], weight.shape[0]
+    M = x.numel() // max(K, 1)
+    if (K == 320 and N <= 640 and M >= 65536 and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and x.is_cuda and not torch.is_grad_enabled() and x.is_contiguous() and weight.is_contiguous()
+            and (bias is None or bias.dtype == x.dtype) and N % 160 == 0):
+        y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
+        a = _lib.ConvArgs(_ptr(x), _ptr(weight), _ptr(bias), None, _ptr(y), 1, M, 1, K, N, M, 1, 1, 1, 0,
+                          _lib.BF16, _lib.CONV_EPI_NONE)
+        check(_lib.load().vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd(linear)")
+        return y
+    return F.linear(x, weight, bias)
 
 
 def linear_residual_supported(x: torch.Tensor, weight: torch.Tensor, residual: torch.Tensor) -> bool:

@@ -289,7 +289,7 @@ class Transformer3DModel(nn.Module):
         Bf, C, H, W = x.shape
         h = group_norm_frames(x, self.norm, 1)
         tok = h.permute(0, 2, 3, 1).reshape(Bf, H * W, C)
-        tok = F.linear(tok, self.proj_in.weight.view(self.proj_in.out_channels, -1), self.proj_in.bias)
+        tok = ops.linear(tok, self.proj_in.weight.view(self.proj_in.out_channels, -1), self.proj_in.bias)
         for blk in self.transformer_blocks:
             tok = blk(tok, context, frames)
         w_out = self.proj_out.weight.view(self.proj_out.out_channels, -1)
