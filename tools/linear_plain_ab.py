@@ -29,7 +29,10 @@ def med(fn, n=20):
 
 rows = []
 with torch.no_grad():
-    for M, K, N in ((131072, 320, 320), (131072, 320, 640), (32768, 640, 640)):
+    shapes = ((131072, 320, 320), (131072, 320, 640), (32768, 640, 640))
+    if len(sys.argv) > 2:
+        shapes = tuple(tuple(int(v) for v in a.split("x")) for a in sys.argv[2:])
+    for M, K, N in shapes:
         x = torch.randn(M, K, device="cuda").bfloat16()
         w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
         b = (torch.randn(N, device="cuda") * 0.1).bfloat16()

@@ -762,6 +762,9 @@ def linear_residual(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.
     return y
 
 
+LINEAR_K10_MAX_N = int(os.environ.get("VP2P_LINEAR_K10_MAX_N", "640"))    # A/B knob, read once
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x @ W^T + b (nn.Linear).  The K = 320 projections of the 64x64 latents (M >= 64k rows, N <= 640:
     attn2's to_q and Transformer3DModel.proj_in at res-64) run on K10's GEMM core, measured faster than
@@ -769,7 +772,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
     a gradient, stays on hipBLASLt (F.linear).  A fixed shape rule: the same kernel every run."""
     K, N = x.shape[-1], weight.shape[0]
     M = x.numel() // max(K, 1)
-    if (K == 320 and N <= 640 and M >= 65536 and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+    if (K == 320 and N <= LINEAR_K10_MAX_N and M >= 65536 and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
             and x.is_cuda and not torch.is_grad_enabled() and x.is_contiguous() and weight.is_contiguous()
             and (bias is None or bias.dtype == x.dtype) and N % 160 == 0):
         y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
