@@ -349,7 +349,10 @@ struct CrossV3Cfg {
   static constexpr int LDS = (KP * KROW + C::DV * VROW) * 2;
 };
 
-template <int D, int KB>
+// T77: the SD text context (77 tokens, KB = 3): in the last 32-key block only keys 64..76 are real,
+// so accumulator registers 8..15 (keys 80..95 for both lane halves) are never computed through exp
+// and the block's second PV k-step (keys 80..95) is skipped.
+template <int D, int KB, bool T77 = false>
 __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(const vp2p_cross_attn_args a, int iters, int b0) {
   using T = bf16;
   using M = Mfma<T>;
@@ -447,6 +450,7 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
+        if (T77 && kb == KB - 1 && i >= 8) continue;
         if (kb == KB - 1 && kb * 32 + acc_row(i, h) >= NKV) sc[kb][i] = kNegInf;
         mx = fmaxf(mx, sc[kb][i]);
       }
@@ -456,6 +460,10 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
+        if (T77 && kb == KB - 1 && i >= 8) {
+          sc[kb][i] = 0.f;
+          continue;
+        }
         const float e = fast_exp2(__builtin_fmaf(sc[kb][i], cs, -mx));
         sc[kb][i] = e;
         sum += e;
@@ -509,8 +517,10 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int sp = 0; sp < 2; ++sp)
+        for (int sp = 0; sp < 2; ++sp) {
+          if (T77 && kb == KB - 1 && sp == 1) continue;     // keys 80..95: no context tokens
           o = M::mma(*reinterpret_cast<const bf16x8*>(Vs + (32 * t + r) * V3::VROW + kb * 32 + 16 * sp + 8 * h), pf[kb][sp], o);
+        }
       __builtin_amdgcn_sched_barrier(0);
       if (qv) {
 #pragma unroll
@@ -588,9 +598,14 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
     const size_t lds = (size_t)V3::LDS + (size_t)sets * a->tokens_kv * sizeof(float);
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    if (!attr || lds > 160 * 1024) return VP2P_E_LAUNCH;
-    hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB>), dim3((unsigned)nx, (unsigned)rows, (unsigned)a->heads),
-                       dim3(256), lds, s, *a, iters, b0);
+    static const bool attr77 = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    if (!attr || !attr77 || lds > 160 * 1024) return VP2P_E_LAUNCH;
+    const dim3 grid((unsigned)nx, (unsigned)rows, (unsigned)a->heads);
+    if (KB == 3 && a->tokens_kv == 77)
+      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true>), grid, dim3(256), lds, s, *a, iters, b0);
+    else
+      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB>), grid, dim3(256), lds, s, *a, iters, b0);
     return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
   };
   int g_first = 0;              // first CFG half / batch row the v1 kernel takes
