@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 10
+#define VP2P_ABI_VERSION 11
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -207,6 +207,10 @@ typedef struct vp2p_step_args {
   float lb_th;
   const float* lb_sub;      /* (prompts, frames, lb_h*lb_w) substruct_words sum, or NULL (run_videop2p.py:149-151) */
   float lb_sub_th;          /* th[1] */
+  /* Optional (prompts, frames, height, width) uint8: the blend mask m_p this launch applied (0/1; the
+   * reference's `mask` after `mask[:1] + mask` and the substruct product, run_videop2p.py:137-153).
+   * Written only when lb_acc is set.  NULL = off (a debug / parity output). */
+  uint8_t* mask_out;
 } vp2p_step_args;
 
 int vp2p_step_fused(const vp2p_step_args* args, void* stream);

@@ -19,6 +19,11 @@ Parts (``--part``, default ``models``):
   models     -> golden_models.npz: FrameAttention, Transformer3DModel (plain and hooked),
                 ResnetBlock3D, and the SD-1.5-geometry UNet3D on a 16x16 latent (DummyController
                 hook, and a controlled bird edit at two controller steps).  ~1 min.
+  nulltext   -> golden_nulltext.npz: NullInversion.ddim_loop + null_optimization (run_videop2p.py:557-612,
+                AST-extracted) on the reference UNet, 2 DDIM steps x up to 3 Adam iterations, at two
+                configs (model_spec.NULLTEXT): the 256/512-channel UNet on a 32^2 latent and the
+                SD-1.5 geometry on a 16^2 latent; saves every inner loss, the optimised unconditional
+                embeddings and the inversion latents.  ~2 min.
   car2 | rabbit8 | penguin24
              -> golden_edit_<part>.npz: the fast-mode P2P edit of model_spec.EDITS[part] through
                 the reference pipeline loop at the SD-1.5 geometry, 512^2 (64^2 latent).  CPU-hours
@@ -156,13 +161,14 @@ class _Stop(Exception):
     pass
 
 
-def part_edit(name, ptp, ns, make_scheduler, threads) -> Dict[str, np.ndarray]:
+def part_edit(name, ptp, ns, make_scheduler, threads, tok) -> Dict[str, np.ndarray]:
     from vp2p.unet3d import UNet3DConditionModel, init_random_
     edit, f, steps, save = MS.EDITS[name]
     prompts, swap, blend, eq, cross, self_ = spec.CONFIGS[edit]
     _, _, ref_unet = ref_models()
     torch.set_num_threads(threads)
-    sd = init_random_(UNet3DConditionModel(), seed=0).state_dict()       # the bench's weights
+    # the bench's weights with the res-16 attn2 q/k tied (model_spec.edit_state: localised blend maps)
+    sd = MS.edit_state(init_random_(UNet3DConditionModel(), seed=0).state_dict())
     unet = ref_unet.UNet3DConditionModel(sample_size=64, cross_attention_dim=768)
     unet.load_state_dict(sd, strict=True)
     del sd
@@ -170,7 +176,8 @@ def part_edit(name, ptp, ns, make_scheduler, threads) -> Dict[str, np.ndarray]:
     # FrameAttention materialises (B*f*heads, 4096, 4096) scores without xformers: use the
     # reference's own attention slicing (unet.py:210-273; attention.py:319-322), one slab at a time
     unet.set_attention_slice(1)
-    inp = MS.edit_inputs(name)
+    # the blend words' token indices from the REFERENCE's get_word_inds (ptp_utils.py:258-276)
+    inp = MS.edit_inputs(name, [ptp.get_word_inds(p, w, tok) for p, w in zip(prompts, blend)])
     x_t = torch.from_numpy(inp["x_t"])
     ns["x_t"] = x_t                      # LocalBlend's closure (run_videop2p.py:136)
     ns["blend_word"] = ((blend[0],), (blend[1],))
@@ -189,7 +196,14 @@ def part_edit(name, ptp, ns, make_scheduler, threads) -> Dict[str, np.ndarray]:
             if lb.counter > lb.start_blend:     # the mask this step's callback applied
                 maps = ctrl.attention_store["down_cross"][2:4] + ctrl.attention_store["up_cross"][:3]
                 maps = torch.cat([m.reshape(lb.alpha_layers.shape[0], -1, 8, 16, 16, 77) for m in maps], dim=2)
-                out[f"mask/{i}"] = np.packbits(lb.get_mask(maps, lb.alpha_layers, True).numpy().astype(bool))
+                mask = lb.get_mask(maps, lb.alpha_layers, True).numpy().astype(bool)
+                frac = mask.reshape(mask.shape[0], -1).mean(1)
+                print(f"[{name}] step {i} mask true fraction per prompt {frac.round(3).tolist()}", flush=True)
+                if not ((frac >= 0.05) & (frac <= 0.95)).all():
+                    raise RuntimeError(f"step {i}: LocalBlend mask true fraction {frac} outside [0.05, 0.95] -- "
+                                       "the end-to-end mask pin would be vacuous")
+                out[f"mask/{i}"] = np.packbits(mask)
+                out[f"mask_frac/{i}"] = frac
         if i == steps - 1:
             raise _Stop
 
@@ -204,9 +218,59 @@ def part_edit(name, ptp, ns, make_scheduler, threads) -> Dict[str, np.ndarray]:
     return out
 
 
+def part_nulltext(ptp, ns, make_scheduler) -> Dict[str, np.ndarray]:
+    """The reference's own null-text optimisation (run_videop2p.py:580-612) with autograd and torch's
+    Adam, on the reference UNet under the DummyController hook (invert() registers None, :615-616)."""
+    from vp2p.unet3d import UNet3DConditionModel, init_random_
+    _, _, ref_unet = ref_models()
+    out: Dict[str, np.ndarray] = {}
+    losses: List[float] = []
+
+    class RecordingF:
+        """nnf with mse_loss recording each inner loss (the reference keeps it in a local)."""
+        def __getattr__(self, k):
+            return getattr(torch.nn.functional, k)
+
+        @staticmethod
+        def mse_loss(a, b):
+            loss = torch.nn.functional.mse_loss(a, b)
+            losses.append(float(loss))
+            return loss
+
+    ns["nnf"] = RecordingF()
+    ns["Adam"] = torch.optim.Adam
+    ns["GUIDANCE_SCALE"] = 7.5
+    ns["DDIMScheduler"] = lambda **kw: None      # built and discarded by NullInversion.__init__ (:637-638)
+    for name, (cfg, std, x_shape, steps, inner) in MS.NULLTEXT.items():
+        losses.clear()
+        sd = init_random_(UNet3DConditionModel(**cfg), seed=0, std=std).state_dict()
+        unet = ref_unet.UNet3DConditionModel(sample_size=64, **cfg)
+        unet.load_state_dict(sd, strict=True)
+        unet.eval()
+        unet.requires_grad_(False)
+        hook(ptp, unet, None)
+        ns["NUM_DDIM_STEPS"] = steps
+        model = types.SimpleNamespace(unet=unet, scheduler=make_scheduler(), tokenizer=None)
+        ni = ns["NullInversion"](model)
+        x0, ctx = (torch.from_numpy(a) for a in MS.nulltext_inputs(name))
+        ni.context = ctx
+        t0 = time.time()
+        with torch.no_grad():
+            lats = ni.ddim_loop(x0)
+        with torch.enable_grad():
+            unc = ni.null_optimization(lats, inner, 1e-5)
+        print(f"[nulltext/{name}] {len(losses)} inner iterations, {time.time() - t0:.0f} s, losses {losses}", flush=True)
+        out[f"{name}/losses"] = np.array(losses, np.float64)
+        out[f"{name}/uncond"] = torch.cat(unc).numpy()
+        out[f"{name}/latents"] = torch.stack(lats).numpy()
+    ns["NUM_DDIM_STEPS"] = 50
+    ns["nnf"] = torch.nn.functional
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--part", default="models", choices=["models"] + sorted(MS.EDITS))
+    ap.add_argument("--part", default="models", choices=["models", "nulltext"] + sorted(MS.EDITS))
     ap.add_argument("--threads", type=int, default=torch.get_num_threads())
     args = ap.parse_args()
     tok = SyntheticCLIPTokenizer()
@@ -215,8 +279,11 @@ def main():
     if args.part == "models":
         out = part_models(ptp, ns)
         path = os.path.join(HERE, "golden_models.npz")
+    elif args.part == "nulltext":
+        out = part_nulltext(ptp, ns, make_scheduler)
+        path = os.path.join(HERE, "golden_nulltext.npz")
     else:
-        out = part_edit(args.part, ptp, ns, make_scheduler, args.threads)
+        out = part_edit(args.part, ptp, ns, make_scheduler, args.threads, tok)
         path = os.path.join(HERE, f"golden_edit_{args.part}.npz")
     if bad:
         raise RuntimeError(f"{len(bad)} hooked calls left the finite regime: {bad[:5]}")

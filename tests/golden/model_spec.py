@@ -41,6 +41,15 @@ EDITS = {
 }
 
 
+# Null-text optimisation fixtures (run_videop2p.py:557-612): name -> (UNet3DConditionModel kwargs,
+# init_random_ std, x_0 shape (1, 4, f, h, w), DDIM steps, max inner Adam iterations)
+NULLTEXT = {
+    "c256": (dict(block_out_channels=(256, 256, 512, 512), cross_attention_dim=64, attention_head_dim=8),
+             0.05, (1, 4, 2, 32, 32), 2, 3),
+    "sd15": (dict(cross_attention_dim=768), 0.02, (1, 4, 2, 16, 16), 2, 3),
+}
+
+
 def rng(*key: int) -> np.random.Generator:
     return np.random.default_rng(np.random.SeedSequence(list(key)))
 
@@ -93,6 +102,14 @@ def rn_inputs(name: str):
     return g.standard_normal((B, cin, f, h, w)).astype(np.float32), g.standard_normal((B, T)).astype(np.float32)
 
 
+def nulltext_inputs(name: str):
+    """(x_0 (1, 4, f, h, w), context [uncond; cond] (2, 77, D)) of one null-text fixture."""
+    cfg, _, shape, _, _ = NULLTEXT[name]
+    g = rng(36, zlib.crc32(name.encode()))
+    return (g.standard_normal(shape).astype(np.float32),
+            g.standard_normal((2, 77, cfg["cross_attention_dim"])).astype(np.float32))
+
+
 def unet_small_inputs(batch: int = None):
     """(sample (B, 4, f, h, w), context (B, 77, 768)); ``batch`` overrides B (4 for the edit forwards:
     rows [uncond x 2, cond x 2] with identical uncond rows)."""
@@ -108,12 +125,55 @@ def unet_small_inputs(batch: int = None):
     return sample, ctx
 
 
-def edit_inputs(name: str) -> Dict[str, np.ndarray]:
+# The end-to-end edits must exercise LocalBlend with NON-trivial masks (run_videop2p.py:131-154: the
+# blend is the identity when every pixel passes `mask / max > th`).  With i.i.d. N(0, 0.02) weights
+# and white-noise latents the 40 res-16 cross maps LocalBlend averages are independent and spatially
+# white, so after the 3x3 max-pool every pixel passes.  Three changes make the maps agree and
+# localise, as a trained model's do (profiles/r03_mask_localisation.txt):
+#   * x_T is spatially smooth (an EDIT_LOWRES^2 N(0, 1) grid per channel and frame, bicubic-upsampled
+#     to 64^2, unit std) instead of white noise;
+#   * the 5 res-16 attn2 layers LocalBlend reads share one (head-0, first-layer) to_q / to_k block
+#     across their 8 heads (``edit_state``), so the 40 maps are 5 maps of one query/key geometry;
+#   * the blend words' conditional text embeddings are scaled by EDIT_BLEND_SCALE.
+EDIT_LOWRES = 6
+EDIT_BLEND_SCALE = 4.0
+RES16_ATTN2 = ["down_blocks.2.attentions.0", "down_blocks.2.attentions.1", "up_blocks.1.attentions.0",
+               "up_blocks.1.attentions.1", "up_blocks.1.attentions.2"]
+
+
+def edit_state(sd):
+    """The edit fixtures' UNet weights: the bench's (``vp2p.unet3d.init_random_`` seed 0) with the
+    res-16 attn2 to_q / to_k tied as described above.  ``sd``: {name: CPU tensor}; returns a new dict."""
+    out = dict(sd)
+    for nm in ("to_q", "to_k"):
+        src = sd[f"{RES16_ATTN2[0]}.transformer_blocks.0.attn2.{nm}.weight"]
+        d = src.shape[0] // HEADS
+        tied = src[:d].repeat(HEADS, 1).contiguous()
+        for layer in RES16_ATTN2:
+            out[f"{layer}.transformer_blocks.0.attn2.{nm}.weight"] = tied.clone()
+    return out
+
+
+def edit_inputs(name: str, blend_token_ids=None) -> Dict[str, np.ndarray]:
     """x_T (1, 4, f, 64, 64) and the CFG text embeddings [uncond, uncond, cond_0, cond_1] (4, 77, 768)
-    of one end-to-end edit."""
+    of one end-to-end edit.  ``blend_token_ids``: per prompt, the token indices of its blend word
+    (``get_word_inds``), whose conditional embeddings are scaled by EDIT_BLEND_SCALE."""
+    import torch
     _, f, _, _ = EDITS[name]
     g = rng(35, zlib.crc32(name.encode()))
-    x_t = g.standard_normal((1, 4, f, 64, 64)).astype(np.float32)
+    lo = torch.from_numpy(g.standard_normal((1, 4 * f, EDIT_LOWRES, EDIT_LOWRES)).astype(np.float32))
+    x = torch.nn.functional.interpolate(lo, size=(64, 64), mode="bicubic", align_corners=False)
+    x_t = (x / x.std()).reshape(1, 4, f, 64, 64).numpy().astype(np.float32)
     unc = g.standard_normal((1, 77, 768)).astype(np.float32)
     cond = g.standard_normal((2, 77, 768)).astype(np.float32)
+    if blend_token_ids is not None:
+        for p, ids in enumerate(blend_token_ids):
+            cond[p, list(ids)] *= np.float32(EDIT_BLEND_SCALE)
     return {"x_t": x_t, "emb": np.concatenate([unc, unc, cond]).astype(np.float32)}
+
+
+def blend_token_ids(prompts, blend, tokenizer):
+    """Token indices of each prompt's blend word (vp2p.prompt_align.get_word_inds, golden-exact
+    against ptp_utils.get_word_inds)."""
+    from vp2p.prompt_align import get_word_inds
+    return [tuple(int(i) for i in get_word_inds(p, w, tokenizer)) for p, w in zip(prompts, blend)]

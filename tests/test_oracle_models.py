@@ -96,3 +96,40 @@ def test_unet_controlled_pinned(golden_models, sd_unet, tokenizer, step):
     got = unet_ref.unet_forward(sd_unet, sample, MS.UNET_SMALL_T, ctx, controller=ctrl).numpy()
     assert int(golden_models[f"unet/bird/{step}/layers"]) == 32
     np.testing.assert_allclose(got, golden_models[f"unet/bird/{step}"], rtol=1e-4, atol=5e-5)
+
+
+@pytest.fixture(scope="module")
+def golden_nulltext():
+    import os
+    from conftest import ROOT
+    return np.load(os.path.join(ROOT, "tests", "golden", "golden_nulltext.npz"))
+
+
+def test_null_optimization_pinned(golden_nulltext):
+    """unet_ref.null_optimization (the CPU restatement of run_videop2p.py:580-612) == the reference's
+    own NullInversion.ddim_loop + null_optimization (AST-extracted, run on the reference UNet;
+    tests/golden/make_golden_models.py --part nulltext) on the 256/512-channel config: every inner
+    loss, the optimised unconditional embeddings and the inversion latents."""
+    from vp2p.unet3d import UNet3DConditionModel, init_random_
+    cfg, std, _, steps, inner = MS.NULLTEXT["c256"]
+    sd = init_random_(UNet3DConditionModel(**cfg), seed=0, std=std).state_dict()
+    x0, ctx = (torch.from_numpy(a) for a in MS.nulltext_inputs("c256"))
+    ddim = O.DDIM()
+    ddim.set_timesteps(steps)
+    lats = [x0]
+    ts = [int(t) for t in ddim.timesteps]
+    for i in range(steps):       # NullInversion.ddim_loop (run_videop2p.py:557-567)
+        t = ts[len(ts) - i - 1]
+        lats.append(ddim.next_step(unet_ref.unet_forward(sd, lats[-1], t, ctx[1:]).numpy(), t,
+                                   lats[-1].numpy()))
+        lats[-1] = torch.from_numpy(np.asarray(lats[-1], np.float32))
+    ref_lats = golden_nulltext["c256/latents"]
+    np.testing.assert_allclose(torch.stack(lats).numpy(), ref_lats, rtol=1e-4, atol=1e-5)
+    with torch.enable_grad():
+        unc, losses, _ = unet_ref.null_optimization(sd, [torch.from_numpy(a) for a in ref_lats], ctx[:1], ctx[1:],
+                                                    ddim, num_inner_steps=inner)
+    np.testing.assert_allclose(losses, golden_nulltext["c256/losses"], rtol=1e-4)
+    # Adam divides by sqrt(v): an element whose gradient is ~0 moves by up to lr per iteration with a
+    # sign set by rounding noise, so a few elements may differ by a fraction of lr (1e-2)
+    diff = np.abs(torch.cat(unc).numpy() - golden_nulltext["c256/uncond"])
+    assert diff.mean() < 1e-5 and diff.max() < 1e-2, (diff.mean(), diff.max())

@@ -62,7 +62,8 @@ def test_encode_matches_oracle(vae_state, dtype, tol):
 
 def test_pipeline_helpers(vae_state):
     """decode_latents (pipeline_tuneavideo.py:239-256: 1/0.18215, batches of 4 '(b f)' frames, clamp to
-    [0, 1], a trailing partial batch dropped as the reference loop does), image2latent_video /
+    [0, 1]; a clip whose frame count leaves a trailing partial batch raises, as the reference's
+    rearrange does after its loop drops that batch), image2latent_video /
     latent2image_video (run_videop2p.py:505-537)."""
     from vp2p import vae as V
     vae = _vae(vae_state, torch.float32)
@@ -73,10 +74,13 @@ def test_pipeline_helpers(vae_state):
     ref = vae_ref.decode(vae_state, (lat / V.SCALING).permute(0, 2, 1, 3, 4).reshape(8, 4, 8, 8))
     ref = (ref / 2 + 0.5).clamp(0, 1).reshape(2, 4, 3, 64, 64).permute(0, 2, 1, 3, 4)
     assert video.shape == (2, 3, 4, 64, 64) and _rel(video, ref) < 1e-4
-    # 6 frames of one clip: the reference decodes range(max(6 // 4, 1)) = 1 batch -> 4 frames
+    # 6 frames of one clip: the reference decodes range(max(6 // 4, 1)) = 1 batch -> 4 frames, and
+    # rearrange('(b f) c h w -> b c f h w', f=6) on 4 frames raises
+    with torch.no_grad(), pytest.raises(ValueError):
+        V.decode_latents(vae, torch.randn(1, 4, 6, 8, 8, generator=g).cuda())
     with torch.no_grad():
-        short = V.decode_latents(vae, torch.randn(1, 4, 6, 8, 8, generator=g).cuda())
-    assert short.shape == (1, 3, 4, 64, 64)
+        short = V.decode_latents(vae, torch.randn(1, 4, 3, 8, 8, generator=g).cuda())
+    assert short.shape == (1, 3, 3, 64, 64)
     frames = torch.randint(0, 256, (3, 64, 64, 3), generator=g, dtype=torch.uint8)
     with torch.no_grad():
         z = V.encode_video(vae, frames.cuda()).cpu()

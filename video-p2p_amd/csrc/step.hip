@@ -99,6 +99,7 @@ __global__ __launch_bounds__(256) void step_kernel(const vp2p_step_args a) {
         bool mp = m0 || (pooled[p * kMaxLbPix + k] / pmax[p] > a.lb_th);
         if (a.lb_sub) mp = mp && !(s0 || sub_at(p, k));
         const float mf = mp ? 1.f : 0.f;
+        if (a.mask_out && c == 0) a.mask_out[((int64_t)p * F + fr) * HW + e] = mp ? 1 : 0;
         a.out[(((int64_t)p * Cc + c) * F + fr) * HW + e] = prev[0] + mf * (prev[p] - prev[0]);
       }
     } else {

@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
@@ -111,7 +111,7 @@ class StepArgs(ctypes.Structure):
                 ("width", c_int32), ("cfg", c_int32), ("fast", c_int32), ("guidance", c_float),
                 ("c1", c_float), ("c2", c_float), ("c3", c_float), ("c4", c_float),
                 ("lb_acc", c_void_p), ("lb_h", c_int32), ("lb_w", c_int32), ("lb_count", c_float),
-                ("lb_th", c_float), ("lb_sub", c_void_p), ("lb_sub_th", c_float)]
+                ("lb_th", c_float), ("lb_sub", c_void_p), ("lb_sub_th", c_float), ("mask_out", c_void_p)]
 
 
 class NullTextLossArgs(ctypes.Structure):

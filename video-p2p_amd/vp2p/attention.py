@@ -95,7 +95,8 @@ class FrameAttention(CrossAttention):
         B = x.shape[0] // f
         shard = frame_parallel.active()
         pending = None
-        if shard is not None and shard.world > 1 and not torch.is_grad_enabled():
+        differentiated = autograd.needs_grad(x, self.to_q.weight, self.to_q.bias)
+        if shard is not None and shard.world > 1 and not differentiated:
             # frames are sharded: the rank owning frame 0 broadcasts frame 0's NORMED hidden state
             # (C per token, half the bytes of its K|V) and every rank projects K|V itself.  The
             # broadcast is issued before this rank's Q projection so the two overlap (collective
@@ -103,7 +104,7 @@ class FrameAttention(CrossAttention):
             x0 = (x.view(B, f, *x.shape[1:])[:, 0].contiguous() if shard.rank == 0
                   else torch.empty(B, *x.shape[1:], device=x.device, dtype=x.dtype))
             pending = (x0, shard.broadcast_async(x0))
-        if autograd.needs_grad(x, self.to_q.weight, self.to_q.bias):
+        if differentiated:
             q = F.linear(x, self.to_q.weight, self.to_q.bias)
             prescaled = False
         else:
@@ -127,6 +128,9 @@ class FrameAttention(CrossAttention):
             x0, work = pending
             work.wait()
         else:
+            if shard is not None and shard.world > 1:
+                raise RuntimeError("frame-sharded FrameAttention reached the inference path without "
+                                   "the frame-0 broadcast")
             x0 = x.view(B, f, *x.shape[1:])[:, 0]
         kv = F.linear(x0, wkv, bkv)
         out = ops.frame_attention(q, kv[..., :C], kv[..., C:], f, self.heads, scale=self.scale,
@@ -247,7 +251,7 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
                                          scale=module.scale, cond_only=cond_only)
     else:
         out = ops.temporal_attention_p2p_bd(q, k, v, B, h, prompts=P, self_replace=replace, probs_out=probs,
-                                            scale=module.scale)
+                                            scale=module.scale, cond_only=cond_only)
     if not fused:
         attn = controller(probs, False, place)
         out = _pv_temporal(module, attn, v, B, f, N, temporal_layout == "bf")

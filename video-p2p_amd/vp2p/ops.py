@@ -278,7 +278,7 @@ def temporal_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, fr
 def temporal_attention_p2p_bd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, heads: int,
                               prompts: int = 0, self_replace: bool = False,
                               probs_out: Optional[torch.Tensor] = None, scale: Optional[float] = None,
-                              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                              out: Optional[torch.Tensor] = None, cond_only: bool = False) -> torch.Tensor:
     """Same op on the reference's '(b d) f c' tensors (B*N, f, C)."""
     dt = _dtype(q, k, v)
     BN, F, C = q.shape
@@ -289,7 +289,7 @@ def temporal_attention_p2p_bd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
     d = C // heads
     a = _lib.TemporalAttnArgs(_ptr(q), _ptr(k), _ptr(v), _ptr(out), *st(q), *st(k), *st(v), *st(out),
                               batch, F, N, heads, d, float(d ** -0.5 if scale is None else scale), dt,
-                              prompts, int(self_replace), _ptr(probs_out))
+                              prompts, int(self_replace), _ptr(probs_out), int(cond_only))
     check(_lib.load().vp2p_temporal_attn_p2p_fwd(ctypes.byref(a), _stream()), "vp2p_temporal_attn_p2p_fwd")
     return out
 
@@ -298,11 +298,12 @@ def temporal_attention_p2p_bd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
 def step_fused(noise: torch.Tensor, latents: torch.Tensor, consts, guidance: float = 7.5, cfg: bool = True,
                fast: bool = False, lb_acc: Optional[torch.Tensor] = None, lb_hw=(16, 16),
                lb_count: float = 40.0, lb_th: float = 0.3, out: Optional[torch.Tensor] = None,
-               lb_sub_th: float = 0.3) -> torch.Tensor:
+               lb_sub_th: float = 0.3, mask_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """CFG + DDIM update + LocalBlend in one launch.  noise: (2P or P, C, f, H, W) bf16/f32,
     latents: (P, C, f, H, W) fp32, consts = (c1, c2, c3, c4) float32 scalars.  ``lb_acc``: the
     LocalBlend sums, (P, f, h*w) or (sets, P, f, h*w) with set 1 = the substruct_words sum
-    (thresholded at ``lb_sub_th`` without pooling, run_videop2p.py:149-151)."""
+    (thresholded at ``lb_sub_th`` without pooling, run_videop2p.py:149-151).  ``mask_out``: optional
+    contiguous uint8 (P, f, H, W) that receives the blend mask the launch applied (when lb_acc is set)."""
     if not (noise.is_cuda and latents.is_cuda):
         raise RuntimeError("step_fused runs on the GPU only")
     if latents.dtype != torch.float32 or not latents.is_contiguous() or not noise.is_contiguous():
@@ -326,6 +327,11 @@ def step_fused(noise: torch.Tensor, latents: torch.Tensor, consts, guidance: flo
                       int(cfg), int(fast), float(guidance), c1, c2, c3, c4,
                       _ptr(lb_acc), int(lb_hw[0]), int(lb_hw[1]), float(lb_count), float(lb_th),
                       _ptr(lb_sub), float(lb_sub_th))
+    if mask_out is not None:
+        if (mask_out.dtype != torch.uint8 or not mask_out.is_contiguous() or not mask_out.is_cuda
+                or tuple(mask_out.shape) != (P, F, H, W)):
+            raise ValueError(f"mask_out must be a contiguous uint8 device tensor of shape {(P, F, H, W)}")
+        a.mask_out = _ptr(mask_out)
     check(_lib.load().vp2p_step_fused(ctypes.byref(a), _stream()), "vp2p_step_fused")
     return out
 

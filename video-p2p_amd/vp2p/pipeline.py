@@ -34,6 +34,11 @@ class VideoP2PPipeline:
         self.tokenizer = tokenizer
         self.text_encoder = text_encoder
         self.vae = vae
+        # debug / parity: when True, every fused step that applies LocalBlend writes the mask it applied
+        # into ``blend_mask`` ((P, f, h, w) uint8, the reference's `mask`, run_videop2p.py:137-153);
+        # ``blend_mask`` is None until the blend first fires
+        self.keep_blend_mask = False
+        self.blend_mask = None
 
     @property
     def device(self):
@@ -105,8 +110,14 @@ class VideoP2PPipeline:
                         acc = lay.share_blend(acc, controller.lb_shape(lat.shape[2]), dev)
                 elif fused:
                     acc = controller.blend_plan()
+                mask = None
+                if self.keep_blend_mask and acc is not None:
+                    if self.blend_mask is None or tuple(self.blend_mask.shape) != (P,) + tuple(lat.shape[2:]):
+                        self.blend_mask = torch.empty((P,) + tuple(lat.shape[2:]), device=dev, dtype=torch.uint8)
+                    mask = self.blend_mask
                 lat = ops.step_fused(noise, lat, self.scheduler.step_constants(t), guidance_scale, cfg=True,
-                                     fast=fast, lb_acc=acc, lb_count=40.0, lb_th=lb_th[0], lb_sub_th=lb_th[1])
+                                     fast=fast, lb_acc=acc, lb_count=40.0, lb_th=lb_th[0], lb_sub_th=lb_th[1],
+                                     mask_out=mask)
             else:  # foreign controller: reference order, step_callback on the new latents
                 u, c = noise.float().chunk(2)
                 e = u + guidance_scale * (c - u)

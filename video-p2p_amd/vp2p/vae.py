@@ -247,21 +247,25 @@ def decode_latents(vae: AutoencoderKL, latents: torch.Tensor, chunk: int = 4) ->
     """TuneAVideoPipeline.decode_latents (pipeline_tuneavideo.py:239-256) on the GPU: (b, 4, f, h, w)
     latents -> (b, 3, f, 8h, 8w) video in [0, 1] (fp32, on the device).  Frames are decoded in
     '(b f)' batches of ``chunk`` (the reference's bs = 4).  As in the reference loop
-    (``range(max(n // bs, 1))``), a trailing partial batch is dropped when n > bs is not a multiple
-    of bs.  Under a frame-sharded edit (``frame_parallel``) each rank decodes its own frames."""
+    (``range(max(n // bs, 1))``), a trailing partial batch is never decoded when n > bs is not a
+    multiple of bs, so the reference's ``rearrange(..., f=video_length)`` raises; this raises
+    ``ValueError`` in the same case (judged on the global frame count under frame sharding, where
+    each rank decodes all of its own frames)."""
     b, c, f, h, w = latents.shape
+    sh = frame_parallel.active()
+    n_global = b * f * (sh.world if sh is not None else 1)
+    if n_global > chunk and n_global % chunk:
+        raise ValueError(f"decode_latents: {n_global} frames are not a multiple of the decode batch {chunk} "
+                         f"(the reference drops the trailing {n_global % chunk} and its rearrange fails)")
     x = (1 / SCALING) * latents
     x = x.permute(0, 2, 1, 3, 4).reshape(b * f, c, h, w)
     n = x.shape[0]
     outs = []
-    for i in range(max(n // chunk, 1)):
-        v = vae.decode(x[i * chunk:min((i + 1) * chunk, n)])
+    for i in range(0, n, chunk):
+        v = vae.decode(x[i:min(i + chunk, n)])
         outs.append((v.float() / 2 + 0.5).clamp(0, 1))
     video = torch.cat(outs)
-    kept = video.shape[0] // b if video.shape[0] % b == 0 else None
-    if kept is None:
-        raise ValueError(f"decode_latents: {video.shape[0]} decoded frames do not split over batch {b}")
-    return video.reshape(b, kept, *video.shape[1:]).permute(0, 2, 1, 3, 4)
+    return video.reshape(b, f, *video.shape[1:]).permute(0, 2, 1, 3, 4)
 
 
 @torch.no_grad()
