@@ -219,11 +219,20 @@ def _pmc_traffic(shape):
 # -- CPU baseline -----------------------------------------------------------------------------------------
 def cpu_baseline(frames, ddim_steps, sample_frames=2):
     """The oracle's fp32 CPU UNet (oracle/unet_ref.py: the reference math, pinned to the reference's
-    own model files) for ONE complete UNet forward of the edit (B = 4, every layer: 16 transformer
-    blocks with the controller, 22 resnets, the up/down-sample convs) on ``sample_frames`` frames,
-    timed once on this host's CPU share and extrapolated to ``frames`` x ``ddim_steps``.  Every
-    per-frame cost is linear in the frame count (frame attention reads frame 0's K/V; the temporal
-    f x f attention is < 0.1% of the FLOPs)."""
+    own model files), timed on this host's CPU share on a bounded sample (~30 s) and extrapolated:
+
+    * the edit: ONE complete UNet forward of the edit (B = 4, every layer: 16 transformer blocks with
+      the rabbit controller, 22 resnets, the up/down-sample convs) on ``sample_frames`` frames,
+      x frames/sample_frames x ddim_steps (the headline unit, edited frames/s);
+    * the inversion: one B = 1 forward (DummyController hook), x frames/sample_frames x ddim_steps;
+    * per-layer attention: the reference's three attention ops alone at every
+      attention resolution of the edit forward (B = 4, ``sample_frames`` frames): FrameAttention
+      (attention.py:273-329), the hooked attn2 with the controller and attn_temp
+      (ptp_utils.py:196-221), projections included, one call each.
+
+    Every per-frame cost is linear in the frame count (frame attention reads frame 0's K/V; the
+    temporal f x f attention is < 0.1% of the FLOPs).  Threads: torch's intra-op pool, i.e. the
+    box's OMP_NUM_THREADS (the GPU box allots 16 host threads per GPU; nproc reports the whole host)."""
     from oracle import p2p_oracle as O
     from oracle import unet_ref
     from vp2p.tokenizer import SyntheticCLIPTokenizer
@@ -236,16 +245,47 @@ def cpu_baseline(frames, ddim_steps, sample_frames=2):
     g = torch.Generator().manual_seed(3)
     x = torch.randn(4, 4, sample_frames, 64, 64, generator=g)
     ctx = torch.randn(4, 77, 768, generator=g)
+    scale = frames / sample_frames * ddim_steps
     with torch.no_grad():
         t0 = time.perf_counter()
         unet_ref.unet_forward(sd, x, 981, ctx, ctrl)
         t_fwd = time.perf_counter() - t0
-    t_edit = t_fwd * (frames / sample_frames) * ddim_steps
+        t0 = time.perf_counter()
+        unet_ref.unet_forward(sd, x[:1], 981, ctx[2:3])
+        t_inv = time.perf_counter() - t0
+        ctrl = O.EditController(prompts, swap, {"default_": cross}, self_, SyntheticCLIPTokenizer(),
+                                blend_words=blend, eq_params=eq)
+        layers = {}
+        for res, p, (hw, C) in (("res64", "down_blocks.0.attentions.0.", (4096, 320)),
+                                ("res32", "down_blocks.1.attentions.0.", (1024, 640)),
+                                ("res16", "down_blocks.2.attentions.0.", (256, 1280)),
+                                ("res8", "mid_block.attentions.0.", (64, 1280))):
+            q = p + "transformer_blocks.0."
+            xt = torch.randn(4 * sample_frames, hw, C, generator=g)
+            ms = {}
+            t0 = time.perf_counter()
+            unet_ref.frame_attention(sd, q + "attn1.", xt, sample_frames)
+            ms["frame_attn"] = (time.perf_counter() - t0) * 1e3
+            t0 = time.perf_counter()
+            unet_ref.hooked(sd, q + "attn2.", xt, ctx.repeat_interleave(sample_frames, 0), ctrl, "down")
+            ms["cross_attn_p2p"] = (time.perf_counter() - t0) * 1e3
+            xtt = xt.reshape(4, sample_frames, hw, C).permute(0, 2, 1, 3).reshape(4 * hw, sample_frames, C)
+            t0 = time.perf_counter()
+            unet_ref.hooked(sd, q + "attn_temp.", xtt, None, ctrl, "down")
+            ms["temporal_attn_p2p"] = (time.perf_counter() - t0) * 1e3
+            layers[res] = {k: round(v, 1) for k, v in ms.items()}
+    t_edit = t_fwd * scale
     return {"value": round(frames / t_edit, 6), "unit": "edited frames/s", "cores": threads, "kind": "port",
             "sample": (f"oracle/unet_ref.py fp32 (pinned to tuneavideo's model files): one full UNet3D forward of the "
                        f"edit (B=4, {sample_frames} frames, 512^2, rabbit controller) timed once ({t_fwd:.1f} s), "
                        f"x{frames / sample_frames:g} frames x {ddim_steps} steps (extrapolated)"),
-            "torch_threads": threads, "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
+            "inversion": {"value": round(frames / (t_inv * scale), 6), "unit": "inverted frames/s",
+                          "sample": f"one B=1 forward on {sample_frames} frames ({t_inv:.1f} s), extrapolated alike"},
+            "attention_layer_ms": {"shape": f"B=4, {sample_frames} frames, one call per op (projections included)",
+                                   **layers},
+            "torch_threads": threads, "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
+            "cores_note": "torch intra-op threads = the box's OMP_NUM_THREADS (16 host threads per GPU on the "
+                          "gpurun box); nproc counts the whole host"}
 
 
 def _cpu_model():

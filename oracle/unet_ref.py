@@ -124,6 +124,77 @@ def transformer(sd, p, x5, ctx, controller, place):
     return h.reshape(B, f, C, H, W).permute(0, 2, 1, 3, 4)
 
 
+def transformer_token_slice(sd, p, x5, ctx, tokens, dtype=torch.float64):
+    """``transformer`` (Transformer3DModel.forward, attention.py:90-137, 233-270; plain attention =
+    the DummyController hook in the finite regime) evaluated only at the spatial positions
+    ``tokens`` (indices into H*W), for every frame: (B, C, f, len(tokens)).
+
+    Exact for a long clip without computing all of it: GroupNorm statistics are per frame over all
+    positions (computed in full), attn1 needs Q at the slice and frame 0's K/V at every position
+    (attention.py:296-302), attn2 and the feed-forward are per position, and attn_temp mixes only the
+    frames of one position (attention.py:262-268).  ``dtype``: arithmetic precision (float64 = an
+    independent high-precision check of the fp32/bf16 kernels)."""
+    B, C, f, H, W = x5.shape
+    sd = {k: v.to(dtype) for k, v in sd.items()}
+    tok = torch.as_tensor(tokens, dtype=torch.int64)
+    S = tok.numel()
+    G = 32
+    xs = torch.empty(B, f, S, C, dtype=dtype)          # x at the slice: (b, f, s, c)
+    hs = torch.empty(B, f, S, C, dtype=dtype)          # GroupNorm(x) at the slice
+    h0 = torch.empty(B, H * W, C, dtype=dtype)         # GroupNorm(x) of frame 0, every position
+    for b in range(B):
+        for fr in range(f):
+            xf = x5[b, :, fr].reshape(C, H * W).to(dtype)
+            g = xf.reshape(G, -1)
+            mean = g.mean(1, keepdim=True)
+            var = g.var(1, unbiased=False, keepdim=True)
+            hn = ((g - mean) / torch.sqrt(var + 1e-6)).reshape(C, H * W)
+            hn = hn * sd[p + "norm.weight"][:, None] + sd[p + "norm.bias"][:, None]
+            xs[b, fr] = xf[:, tok].T
+            hs[b, fr] = hn[:, tok].T
+            if fr == 0:
+                h0[b] = hn.T
+    w_in = sd[p + "proj_in.weight"].reshape(C, C)
+    t = hs @ w_in.T + sd[p + "proj_in.bias"]            # (B, f, S, C)
+    t0 = h0 @ w_in.T + sd[p + "proj_in.bias"]           # (B, HW, C): frame 0, every position
+    q_ = p + "transformer_blocks.0."
+    d = C // HEADS
+
+    def lin(x, name):
+        return F.linear(x, sd[name + "weight"], sd.get(name + "bias"))
+
+    def ln(x, name):
+        return F.layer_norm(x, (C,), sd[name + "weight"], sd[name + "bias"], 1e-5)
+
+    def attend(q, k, v):
+        """q (..., Nq, C), k/v (..., Nk, C): softmax(q k^T d^-1/2) v per head."""
+        qh = q.reshape(*q.shape[:-1], HEADS, d).transpose(-2, -3)
+        kh = k.reshape(*k.shape[:-1], HEADS, d).transpose(-2, -3)
+        vh = v.reshape(*v.shape[:-1], HEADS, d).transpose(-2, -3)
+        a = torch.softmax(qh @ kh.transpose(-1, -2) * d ** -0.5, dim=-1)
+        o = (a @ vh).transpose(-2, -3)
+        return o.reshape(*o.shape[:-2], C)
+
+    a1 = q_ + "attn1."
+    k0 = lin(ln(t0, q_ + "norm1."), a1 + "to_k.")                  # (B, HW, C)
+    v0 = lin(ln(t0, q_ + "norm1."), a1 + "to_v.")
+    qa = lin(ln(t, q_ + "norm1."), a1 + "to_q.")                   # (B, f, S, C)
+    t = lin(attend(qa, k0[:, None], v0[:, None]), a1 + "to_out.0.") + t
+    a2 = q_ + "attn2."
+    c = ctx.to(dtype)[:, None]                                     # (B, 1, 77, D): repeated per frame
+    t = lin(attend(lin(ln(t, q_ + "norm2."), a2 + "to_q."), lin(c, a2 + "to_k."), lin(c, a2 + "to_v.")),
+            a2 + "to_out.0.") + t
+    a, g = lin(ln(t, q_ + "norm3."), q_ + "ff.net.0.proj.").chunk(2, dim=-1)
+    t = lin(a * F.gelu(g), q_ + "ff.net.2.") + t
+    tt = t.transpose(1, 2)                                         # (B, S, f, C): '(b d) f c'
+    n = ln(tt, q_ + "norm_temp.")
+    at = q_ + "attn_temp."
+    tt = lin(attend(lin(n, at + "to_q."), lin(n, at + "to_k."), lin(n, at + "to_v.")), at + "to_out.0.") + tt
+    w_out = sd[p + "proj_out.weight"].reshape(C, C)
+    y = tt @ w_out.T + sd[p + "proj_out.bias"] + xs.transpose(1, 2)     # (B, S, f, C)
+    return y.permute(0, 3, 2, 1)
+
+
 def timestep_embedding(t: torch.Tensor, dim: int = 320) -> torch.Tensor:
     half = dim // 2
     freqs = torch.exp(-math.log(10000) * torch.arange(half, dtype=torch.float32) / half)

@@ -133,3 +133,16 @@ def test_null_optimization_pinned(golden_nulltext):
     # sign set by rounding noise, so a few elements may differ by a fraction of lr (1e-2)
     diff = np.abs(torch.cat(unc).numpy() - golden_nulltext["c256/uncond"])
     assert diff.mean() < 1e-5 and diff.max() < 1e-2, (diff.mean(), diff.max())
+
+
+@pytest.mark.parametrize("name", list(MS.T3D_CONFIGS))
+def test_transformer_token_slice_pinned(golden_models, name):
+    """unet_ref.transformer_token_slice (the long-clip oracle: Transformer3DModel at a few positions of
+    every frame) == the reference Transformer3DModel (attention.py:90-137) at those positions."""
+    B, f, h, w, C, D = MS.T3D_CONFIGS[name]
+    sd = model_state(_t3d_factory(C, D), 42)
+    x, ctx = (torch.from_numpy(a) for a in MS.t3d_inputs(name))
+    tokens = [0, 3, h * w // 2 + 1, h * w - 1]
+    got = unet_ref.transformer_token_slice(sd, "", x, ctx, tokens).numpy()
+    ref = golden_models[f"t3d/{name}/hooked"].reshape(B, C, f, h * w)[..., tokens]
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=5e-5)

@@ -353,7 +353,8 @@ struct CrossV3Cfg {
 // so accumulator registers 8..15 (keys 80..95 for both lane halves) are never computed through exp
 // and the block's second PV k-step (keys 80..95) is skipped.
 template <int D, int KB, bool T77 = false>
-__global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(const vp2p_cross_attn_args a, int iters, int b0) {
+__global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(const vp2p_cross_attn_args a, int iters, int b0,
+                                                                               int nx, int rows) {
   using T = bf16;
   using M = Mfma<T>;
   using C = CrossCfg<T, D>;
@@ -366,8 +367,22 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
   const int FQ = a.frames * a.tokens_q;
   const bool p2p = a.prompts > 0 && a.batch == (a.cond_only ? 1 : 2) * a.prompts;
-  const int b = b0 + (int)blockIdx.y;          // batch row
-  const int head = blockIdx.z;
+  // 1-D grid, XCD-grouped (xcd_remap) with the head fastest: the a.heads workgroups of one query range
+  // run together on ONE XCD, so the 128-B lines their head slices share (d = 40: 80-B slices of
+  // 640-B rows) are fetched into one L2 once and written back whole, not once per XCD / half-written
+  // (r02 PMC: 1.27x the algorithmic bytes with the (x, row, head) 3-D grid).  nx = 0: the 3-D grid.
+  int bx, by, bz;
+  if (nx > 0) {
+    const int lid = xcd_remap((int)blockIdx.x, nx * rows * a.heads);
+    bz = lid % a.heads;
+    const int rest = lid / a.heads;
+    bx = rest % nx;
+    by = rest / nx;
+  } else {
+    bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  }
+  const int b = b0 + by;                       // batch row
+  const int head = bz;
   const int g = p2p ? b / a.prompts : 0;        // CFG half
   const int pw = p2p ? b - g * a.prompts : 0;   // prompt within the half
   const bool cond = p2p && (a.cond_only || g == 1);
@@ -401,7 +416,7 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
   const bool norm_p = lb || a.probs_out;
   // stream w's query blocks: qb0, qb0 + 4, ...; (frame, token) of the lane's query tracked
   // incrementally (no integer division in the loop)
-  const int qb0 = blockIdx.x * 4 * iters + w;
+  const int qb0 = bx * 4 * iters + w;
   constexpr int NS = 4;
   const int step = 32 * NS;
   const T* qbase = static_cast<const T*>(a.q) + b * a.q_sb + head * D;
@@ -538,6 +553,250 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// K2 v3e (bf16, prompts = 2): the EDITED conditional half of an edit launch (run_videop2p.py:304-317:
+// the reference edits attn[h//2:] only), v3-style.  A workgroup is one head of the conditional half:
+// both prompts' K and V^T fragments sit in LDS (staged once), and its 8 waves are 8 query streams.
+// Per query block a wave computes the source prompt (its probabilities parked in the wave's own LDS
+// rows, fp32), then the edited prompt, whose softmax epilogue applies Replace / Refine, Reweight and
+// the word-alpha blend exactly as cross_attn_kernel (v1) does; Q is prefetched one (block, prompt)
+// ahead.  Replaces v1 on these rows (v1: K/V re-read from L2 per item, one item per workgroup).
+// ------------------------------------------------------------------------------------------------
+template <int D, int KB>
+struct CrossV3eCfg {
+  using V3 = CrossV3Cfg<D, KB>;
+  static constexpr int NW = 8;                                   // waves (query streams)
+  static constexpr int KV = 2 * V3::LDS;                         // both prompts' K, V^T
+};
+
+template <int D, int KB, bool T77 = false>
+__global__ __launch_bounds__(512, 1) void cross_attn_kernel_v3e(const vp2p_cross_attn_args a, int iters, int nx, int prow) {
+  using T = bf16;
+  using M = Mfma<T>;
+  using C = CrossCfg<T, D>;
+  using V3 = CrossV3Cfg<D, KB>;
+  using E = CrossV3eCfg<D, KB>;
+  constexpr int KP = V3::KP;
+  constexpr int NW = E::NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int NKV = a.tokens_kv;
+  const int FQ = a.frames * a.tokens_q;
+  const int LBS = a.lb_sets == 2 ? 2 : 1;
+  const bool lb = a.lb_acc != nullptr;
+  // 1-D XCD-grouped grid, head fastest (see cross_attn_kernel_v3)
+  const int lid = xcd_remap((int)blockIdx.x, nx * a.heads);
+  const int head = lid % a.heads, bx = lid / a.heads;
+  const int brow0 = a.cond_only ? 0 : a.prompts;                // batch row of the source prompt
+
+  T* Ks0 = reinterpret_cast<T*>(smem);
+  float* psrc = reinterpret_cast<float*>(smem + E::KV) + (w * 32 + r) * prow;
+  f32x4* etab = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + E::KV) + NW * 32 * prow);
+  float* lbw = reinterpret_cast<float*>(etab + NKV);             // [set][prompt][word]
+
+  // stage both prompts' K [KP][DP] and V^T [DV][KP] (padded rows), the edit table and the LB weights
+  const T* ws = static_cast<const T*>(a.kv_ws);
+  const int64_t kelems = (int64_t)a.batch * a.heads * KP * C::DP;
+  constexpr int KV8 = KP * C::DP / 8, VV8 = C::DV * KP / 8;
+  for (int i = tid; i < 2 * (KV8 + VV8); i += 512) {
+    const int p = i / (KV8 + VV8), j0 = i - p * (KV8 + VV8);
+    const int b = brow0 + p;
+    T* Ks = Ks0 + p * (V3::LDS / 2);
+    T* Vs = Ks + KP * V3::KROW;
+    if (j0 < KV8) {
+      const T* src = ws + ((int64_t)(b * a.heads + head) * KP) * C::DP;
+      const int row = j0 / (C::DP / 8), c = (j0 - row * (C::DP / 8)) * 8;
+      *reinterpret_cast<u32x4*>(Ks + row * V3::KROW + c) = *reinterpret_cast<const u32x4*>(src + row * C::DP + c);
+    } else {
+      const T* src = ws + kelems + ((int64_t)(b * a.heads + head) * KP) * C::DV;
+      const int j = j0 - KV8, row = j / (KP / 8), c = (j - row * (KP / 8)) * 8;
+      *reinterpret_cast<u32x4*>(Vs + row * V3::VROW + c) = *reinterpret_cast<const u32x4*>(src + row * KP + c);
+    }
+  }
+  for (int i = tid; i < NKV; i += 512) {
+    f32x4 t;
+    t[0] = a.edit_mode == VP2P_EDIT_REFINE ? a.refine_alpha[i] : 0.f;
+    t[1] = a.reweight ? a.equalizer[i] : 1.f;
+    t[2] = a.alpha_words[i];
+    t[3] = __int_as_float(a.edit_mode == VP2P_EDIT_REFINE ? a.map_idx[i] : i);
+    etab[i] = t;
+  }
+  if (lb)
+    for (int i = tid; i < LBS * 2 * NKV; i += 512) lbw[i] = a.lb_word_alpha[i];
+  __syncthreads();
+
+  const float cs = a.scale * kLog2e;
+  const int qb0 = bx * NW * iters + w;
+  constexpr int step = 32 * NW;
+  int qi = qb0 * 32 + r;
+  int fr_n = qi / a.tokens_q, pos_n = qi - fr_n * a.tokens_q;
+  auto advance = [&](int& f_, int& p_) {
+    p_ += step;
+    while (p_ >= a.tokens_q) { p_ -= a.tokens_q; ++f_; }
+  };
+  auto load_q = [&](int qi_, int f_, int p_, int prompt, bf16x8* dst) {
+    const bool ok = qi_ < FQ;
+    const T* row = static_cast<const T*>(a.q) + (brow0 + prompt) * a.q_sb + head * D +
+                   (ok ? f_ * a.q_sf + p_ * a.q_sn : 0);
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) dst[s] = ok ? M::row_frag(row, s, h, D) : M::zero();
+  };
+  bf16x8 qn[C::KS];
+  load_q(qi, fr_n, pos_n, 0, qn);
+
+  for (int it = 0; it < iters; ++it) {
+    const int qcur = qi, fcur = fr_n, pcur = pos_n;
+    const bool qv = qcur < FQ;
+    for (int p = 0; p < 2; ++p) {
+      bf16x8 qf[C::KS];
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) qf[s] = qn[s];
+      if (p == 0) {
+        load_q(qcur, fcur, pcur, 1, qn);
+      } else if (it + 1 < iters) {
+        advance(fr_n, pos_n);
+        qi += step;
+        load_q(qi, fr_n, pos_n, 0, qn);
+      }
+      const T* Ks = Ks0 + p * (V3::LDS / 2);
+      const T* Vs = Ks + KP * V3::KROW;
+      f32x16 sc[KB];
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        sc[kb] = zero16();
+#pragma unroll
+        for (int s2 = 0; s2 < C::KS; ++s2)
+          sc[kb] = M::mma(*reinterpret_cast<const bf16x8*>(Ks + (kb * 32 + r) * V3::KROW + 16 * s2 + 8 * h), qf[s2], sc[kb]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // normalised row softmax (the edit reads probabilities: run_videop2p.py:304-317)
+      float mx = kNegInf;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (T77 && kb == KB - 1 && i >= 8) continue;
+          if (kb == KB - 1 && kb * 32 + acc_row(i, h) >= NKV) sc[kb][i] = kNegInf;
+          mx = fmaxf(mx, sc[kb][i]);
+        }
+      mx = fmaxf(mx, xhalf(mx)) * cs;
+      float sum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (T77 && kb == KB - 1 && i >= 8) {
+            sc[kb][i] = 0.f;
+            continue;
+          }
+          const float e = fast_exp2(__builtin_fmaf(sc[kb][i], cs, -mx));
+          sc[kb][i] = e;
+          sum += e;
+        }
+      sum += xhalf(sum);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[kb][i] *= inv;
+
+      if (p == 0) {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) psrc[wd] = sc[kb][i];
+          }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else {
+#pragma clang fp contract(off)
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) {
+              const float pe_val = sc[kb][i];
+              const f32x4 t = etab[wd];
+              float R;
+              if (a.edit_mode == VP2P_EDIT_REPLACE) {
+                float gsum = 0.f;
+                for (int n = a.map_ptr[wd]; n < a.map_ptr[wd + 1]; ++n) gsum += psrc[a.map_idx[n]] * a.map_val[n];
+                R = gsum;
+              } else if (a.edit_mode == VP2P_EDIT_REFINE) {
+                R = psrc[__float_as_int(t[3])] * t[0] + pe_val * (1.f - t[0]);
+              } else {
+                R = psrc[wd];
+              }
+              R = R * t[1];
+              sc[kb][i] = R * t[2] + (1.f - t[2]) * pe_val;
+            }
+          }
+      }
+      if (lb) {
+        for (int set = 0; set < LBS; ++set) {
+          const float* wts = lbw + (set * 2 + p) * NKV;
+          float part = 0.f;
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int wd = kb * 32 + acc_row(i, h);
+              if (wd < NKV) part += wts[wd] * sc[kb][i];
+            }
+          part += xhalf(part);
+          if (h == 0 && qv) a.lb_ws[((int64_t)(set * 2 + p) * a.heads + head) * FQ + qcur] = part;
+        }
+      }
+      if (a.probs_out && qv) {
+        float* prow_out = a.probs_out + ((((int64_t)(brow0 + p) * a.frames + fcur) * a.heads + head) * a.tokens_q + pcur) * NKV;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int wd = kb * 32 + acc_row(i, h);
+            if (wd < NKV) prow_out[wd] = sc[kb][i];
+          }
+      }
+      bf16x8 pf[KB][2];
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        pf[kb][0] = M::p_frag(sc[kb], 0);
+        pf[kb][1] = M::p_frag(sc[kb], 1);
+      }
+      T* orow = static_cast<T*>(a.o) + (brow0 + p) * a.o_sb + head * D + fcur * a.o_sf + pcur * a.o_sn;
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t) {
+        f32x16 o = zero16();
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp) {
+            if (T77 && kb == KB - 1 && sp == 1) continue;
+            o = M::mma(*reinterpret_cast<const bf16x8*>(Vs + (32 * t + r) * V3::VROW + kb * 32 + 16 * sp + 8 * h), pf[kb][sp], o);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+        if (qv) {
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const int dc = 32 * t + 8 * gq + 4 * h;
+            if (dc < D) {
+              bf16x4 v;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (bf16)o[4 * gq + j];
+              *reinterpret_cast<bf16x4*>(orow + dc) = v;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
 // lb_acc[p][qi] += sum over heads (in head order) of lb_ws[p][head][qi]: deterministic, one
 // read-modify-write per (prompt, token).
 __global__ void cross_lb_reduce_kernel(float* __restrict__ lb_acc, const float* __restrict__ lb_ws,
@@ -579,6 +838,24 @@ static int cross_nonedit_kernel() {
   return k;
 }
 
+// VP2P_K2_EDIT=v1: A/B switch of the edited half back to v1 (default v3e), read once
+static int cross_edit_kernel() {
+  static const int k = [] {
+    const char* e = getenv("VP2P_K2_EDIT");
+    return (e && e[0] == 'v' && e[1] == '1') ? 1 : 3;
+  }();
+  return k;
+}
+
+// VP2P_K2_GRID=3d: A/B switch back to v3's (x, row, head) grid (default: 1-D, XCD-grouped), read once
+static bool cross_grid_1d() {
+  static const bool g = [] {
+    const char* e = getenv("VP2P_K2_GRID");
+    return !(e && e[0] == '3');
+  }();
+  return g;
+}
+
 template <typename T, int D, int KB>
 static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
   const int FQ = a->frames * a->tokens_q;
@@ -601,11 +878,41 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
     static const bool attr77 = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true>),
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     if (!attr || !attr77 || lds > 160 * 1024) return VP2P_E_LAUNCH;
-    const dim3 grid((unsigned)nx, (unsigned)rows, (unsigned)a->heads);
+    const bool g1 = cross_grid_1d() && nx * rows * a->heads <= 0x7fffffff;
+    const dim3 grid = g1 ? dim3((unsigned)(nx * rows * a->heads)) : dim3((unsigned)nx, (unsigned)rows, (unsigned)a->heads);
+    const int nx1 = g1 ? (int)nx : 0;
     if (KB == 3 && a->tokens_kv == 77)
-      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true>), grid, dim3(256), lds, s, *a, iters, b0);
+      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows);
     else
-      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB>), grid, dim3(256), lds, s, *a, iters, b0);
+      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows);
+    return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+  };
+  // v3e over the edited conditional half (prompts = 2, bf16); returns VP2P_E_SHAPE to fall back to v1
+  auto launch_v3e = [&]() -> int {
+    using V3 = CrossV3Cfg<D, KB>;
+    using E = CrossV3eCfg<D, KB>;
+    const int prow = a->tokens_kv | 1;
+    const int sets = a->lb_sets == 2 ? 2 : 1;
+    const size_t lds = (size_t)E::KV + (size_t)E::NW * 32 * prow * 4 + (size_t)a->tokens_kv * 16 +
+                       (size_t)sets * 2 * a->tokens_kv * 4;
+    if (lds > 160 * 1024) return VP2P_E_SHAPE;
+    const int64_t qblocks = (FQ + 31) / 32;
+    const int64_t per_wg = (qblocks + E::NW - 1) / E::NW;
+    // ~1 workgroup per CU over the heads; each of its 8 streams then loops `iters` blocks
+    int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (256 + a->heads - 1) / a->heads));
+    const int iters = (int)((per_wg + nx - 1) / nx);
+    nx = (per_wg + iters - 1) / iters;
+    if (nx * a->heads > 0x7fffffff) return VP2P_E_SHAPE;
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3e<D, KB>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    static const bool attr77 = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3e<D, KB, true>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    if (!attr || !attr77) return VP2P_E_LAUNCH;
+    const dim3 grid((unsigned)(nx * a->heads));
+    if (KB == 3 && a->tokens_kv == 77)
+      hipLaunchKernelGGL((cross_attn_kernel_v3e<D, KB, true>), grid, dim3(512), lds, s, *a, iters, (int)nx, prow);
+    else
+      hipLaunchKernelGGL((cross_attn_kernel_v3e<D, KB>), grid, dim3(512), lds, s, *a, iters, (int)nx, prow);
     return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
   };
   int g_first = 0;              // first CFG half / batch row the v1 kernel takes
@@ -616,6 +923,21 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
       const int rc = launch_v3(0, a->prompts);     // the unconditional half: plain attention on v3
       if (rc != VP2P_OK) return rc;
       g_first = 1;
+    }
+    if (edit && a->prompts == 2 && cross_edit_kernel() == 3) {
+      const int rc = launch_v3e();
+      if (rc == VP2P_OK) {
+        if (a->lb_acc) {
+          const int sets = a->lb_sets == 2 ? 2 : 1;
+          const int64_t n = (int64_t)sets * a->prompts * FQ;
+          const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+          hipLaunchKernelGGL(cross_lb_reduce_kernel, dim3(blocks), dim3(256), 0, s, a->lb_acc, a->lb_ws,
+                             sets * a->prompts, a->heads, FQ);
+          if (hipGetLastError() != hipSuccess) return VP2P_E_LAUNCH;
+        }
+        return VP2P_OK;
+      }
+      if (rc != VP2P_E_SHAPE) return rc;
     }
     if (!edit && cross_nonedit_kernel() == 3) {
       const int rc = launch_v3(0, a->batch);

@@ -343,7 +343,7 @@ __device__ __forceinline__ void frame_attn_exact_row(const vp2p_frame_attn_args&
 constexpr int x2f_bufs(int D, int KT, bool FOLD) { return FOLD && D <= 64 && KT <= 128 ? 2 : 1; }
 
 template <int D, int KT, bool FOLD>
-__global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame_attn_args a) {
+__global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame_attn_args a, int head_fastest) {
   constexpr int kK1Bufs = x2f_bufs(D, KT, FOLD);
   using T = bf16;
   using M = Mfma<T>;
@@ -362,8 +362,22 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   const int FQ = a.frames * a.tokens_q;
   const int qblocks = (FQ + 255) >> 8;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = bid / qblocks, qb = bid - bh * qblocks;
-  const int b = bh / a.heads, head = bh - b * a.heads;
+  int b, head, qb;
+  if (head_fastest) {
+    // the a.heads workgroups of one query block are consecutive on one XCD: together their 80-B head
+    // slices cover whole 128-B lines of Q and O, read into and written back from one L2 at once
+    // (query-block-major order: each line is touched by ~2 heads' workgroups at different times)
+    const int per_b = qblocks * a.heads;
+    b = bid / per_b;
+    const int rem = bid - b * per_b;
+    qb = rem / a.heads;
+    head = rem - qb * a.heads;
+  } else {
+    const int bh = bid / qblocks;
+    qb = bid - bh * qblocks;
+    b = bh / a.heads;
+    head = bh - b * a.heads;
+  }
   const int Nk = a.tokens_kv;
   const float cs = a.q_prescaled ? 1.f : a.scale * kLog2e;
 
@@ -621,6 +635,14 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   }
 }
 
+static int k1_head_fastest() {   // VP2P_K1_GRID=bh: A/B switch to the (b, head)-major grid, read once
+  static const int hf = [] {
+    const char* e = getenv("VP2P_K1_GRID");
+    return (e && e[0] == 'b') ? 0 : 1;
+  }();
+  return hf;
+}
+
 static bool x2f_d80_off() {   // VP2P_K1_D80=1set: A/B switch for the res-32 layers, read once
   static const bool off = [] {
     const char* e = getenv("VP2P_K1_D80");
@@ -635,7 +657,8 @@ static int launch_x2f(const vp2p_frame_attn_args* a, int64_t nwg, hipStream_t st
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_x2f<D, KT, FOLD>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  hipLaunchKernelGGL((frame_attn_kernel_x2f<D, KT, FOLD>), dim3((unsigned)nwg), dim3(256), lds, stream, *a);
+  hipLaunchKernelGGL((frame_attn_kernel_x2f<D, KT, FOLD>), dim3((unsigned)nwg), dim3(256), lds, stream, *a,
+                     k1_head_fastest());
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 

@@ -64,9 +64,15 @@ class VideoP2PPipeline:
                  latents: Optional[torch.Tensor] = None, uncond_embeddings_pre=None, controller=None,
                  fast: bool = False, eta: float = 0.0, text_embeddings: Optional[torch.Tensor] = None,
                  generator=None, output_type: str = "latent", callback=None, callback_steps: int = 1,
-                 **kwargs):
+                 graphs: bool = False, **kwargs):
         """``callback(i, t, latents)`` runs after every ``callback_steps``-th step's update (and
-        LocalBlend), as in pipeline_tuneavideo.py:427-430."""
+        LocalBlend), as in pipeline_tuneavideo.py:427-430.
+
+        ``graphs=True``: every denoising step (UNet forward + the fused CFG/DDIM/LocalBlend step) is
+        captured once as a HIP graph and replayed: the first call per (controller, shapes, schedule)
+        captures and then replays, later calls only replay (``_GraphedEdit``).  Results are
+        bit-identical to the eager loop.  Needs a vp2p controller (fused protocol) or none, one
+        process (no frame sharding), no ``keep_blend_mask``."""
         if eta != 0.0:
             raise NotImplementedError("eta > 0 is out of scope (deterministic DDIM only)")
         if output_type not in ("latent", "tensor"):
@@ -83,6 +89,16 @@ class VideoP2PPipeline:
             latents = torch.randn(shape, generator=generator, dtype=torch.float32).to(dev)
         lat = latents.to(dev, torch.float32).expand(shape).contiguous() * self.scheduler.init_noise_sigma
         fused = controller is not None and hasattr(controller, "blend_plan")
+        if graphs:
+            if not (fused or controller is None) or frame_parallel.active_layout() is not None \
+                    or frame_parallel.active() is not None or self.keep_blend_mask:
+                raise NotImplementedError("graphs=True: a vp2p controller (or none), one process, no keep_blend_mask")
+            lat = self._graphed(controller, prompts, lat, emb, num_inference_steps, guidance_scale, fast,
+                                uncond_embeddings_pre, callback, callback_steps)
+            if output_type == "tensor":
+                from .vae import decode_latents
+                return decode_latents(self.vae, lat)
+            return lat
         lb_th = (0.3, 0.3)
         if fused and controller.local_blend is not None:
             lb_th = controller.local_blend.th
@@ -131,6 +147,81 @@ class VideoP2PPipeline:
             from .vae import decode_latents
             return decode_latents(self.vae, lat)
         return lat
+
+
+    def _graphed(self, controller, prompts, lat0, emb0, steps, guidance, fast, uncond_pre, callback, callback_steps):
+        key = (id(controller), tuple(lat0.shape), tuple(emb0.shape), steps, float(guidance), bool(fast),
+               uncond_pre is not None, str(lat0.device))
+        cache = self.__dict__.setdefault("_graph_cache", {})
+        ge = cache.get(key)
+        if ge is None or ge.controller is not controller:
+            ge = cache[key] = _GraphedEdit(self, controller, prompts, lat0, emb0, steps, guidance, fast, uncond_pre)
+        return ge.run(lat0, emb0, uncond_pre, callback, callback_steps)
+
+
+class _GraphedEdit:
+    """One captured edit: a HIP graph per denoising step (pipeline_tuneavideo.py:394-430 body), all
+    in one private memory pool and replayed in capture order.  The per-step scalars (timestep, DDIM
+    constants, the controller's step-dependent edit / self-replace / LocalBlend decisions and its
+    word-alpha row) are baked into step i's graph when it is captured; the tensors a replay reads
+    are static buffers refreshed by ``run``: the initial latents, the text embeddings and the
+    optional per-step unconditional embeddings."""
+
+    def __init__(self, pipe, controller, prompts, lat0, emb0, steps, guidance, fast, uncond_pre):
+        self.controller = controller
+        unet, sched = pipe.unet, pipe.scheduler
+        dev = lat0.device
+        sched.set_timesteps(steps)
+        self.ts = sched.timesteps.tolist()
+        P = len(prompts)
+        self.lat_in = lat0.clone()
+        self.emb = emb0.clone()
+        self.unc = None if uncond_pre is None else torch.stack([u.reshape(self.emb[0].shape) for u in uncond_pre]).to(dev)
+        t_dev = [torch.tensor([t], dtype=torch.int64, device=dev) for t in self.ts]
+        fused = controller is not None
+        lb_th = (0.3, 0.3)
+        if fused:
+            controller.plan(dev)                       # device tables built outside the capture
+            if controller.local_blend is not None:
+                lb_th = controller.local_blend.th
+        # warm-up: one eager forward makes every lazy cache (concatenated weights, kernel attributes,
+        # code objects) before the capture, then the controller starts the edit afresh
+        torch.cuda.synchronize(dev)
+        with torch.no_grad():
+            unet(torch.cat([self.lat_in, self.lat_in]), t_dev[0], encoder_hidden_states=self.emb)
+        if controller is not None:
+            controller.reset()
+        torch.cuda.synchronize(dev)
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs, self.lats = [], []
+        lat = self.lat_in
+        with torch.no_grad():
+            for i, t in enumerate(self.ts):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.pool):
+                    if self.unc is not None:
+                        self.emb[0].copy_(self.unc[i])
+                    noise = unet(torch.cat([lat, lat]), t_dev[i], encoder_hidden_states=self.emb).sample.contiguous()
+                    acc = controller.blend_plan() if fused else None
+                    lat = ops.step_fused(noise, lat, sched.step_constants(t), guidance, cfg=True, fast=fast,
+                                         lb_acc=acc, lb_count=40.0, lb_th=lb_th[0], lb_sub_th=lb_th[1])
+                    del noise
+                self.graphs.append(g)
+                self.lats.append(lat)
+        # buffers the replays write across steps stay referenced for the graphs' lifetime
+        self.keep = [t_dev, None if controller is None else getattr(controller.attention_store, "lb_acc", None)]
+
+    def run(self, lat0, emb0, uncond_pre, callback, callback_steps):
+        if lat0.data_ptr() != self.lat_in.data_ptr():
+            self.lat_in.copy_(lat0)
+        self.emb.copy_(emb0)
+        if uncond_pre is not None:
+            self.unc.copy_(torch.stack([u.reshape(self.emb[0].shape) for u in uncond_pre]))
+        for i, (g, t) in enumerate(zip(self.graphs, self.ts)):
+            g.replay()
+            if callback is not None and i % callback_steps == 0:
+                callback(i, t, self.lats[i])
+        return self.lats[-1].clone()
 
 
 class NullInversion:
