@@ -65,13 +65,34 @@ __device__ __forceinline__ f32x4v mfma16(bf16x8 a, bf16x8 b, f32x4v c) {
 // ------------------------------------------------------------------------------------------------
 __device__ __attribute__((aligned(16))) unsigned int kZero16[4] = {0, 0, 0, 0};
 
-constexpr int GBM = 128, NW = 4;
-constexpr int G_STAGE = (GBM + BN) * BK * 2;                   // bytes per LDS stage (A then B)
-constexpr int G_LDS = 2 * G_STAGE > GBM * CROW * 2 ? 2 * G_STAGE : GBM * CROW * 2;
-constexpr int G_ADMA = GBM / 8 / NW;                           // A DMA instructions per wave per step: 4
-constexpr int G_BDMA = BN / 8 / NW;                            // B: 5
+constexpr int GBM = 128, NW = 4;                               // the split-K / small-M tile
+// TBM = 128: 4 waves (2 x 2 of 64 x 80), two LDS stages, one __syncthreads per K-step, two
+// workgroups per CU.  TBM = 256 ("big"): 8 waves (4 x 2 of 64 x 80), THREE LDS stages (3 x 52 KB),
+// one workgroup per CU; the DMA of steps s+1 and s+2 are in flight under step s's MFMAs (counted
+// vmcnt + raw s_barrier, so the barrier does not drain the ring).  Same per-output K order and
+// MFMA sequence: bit-equal results.
+template <int TBM> struct GCfg {
+  static constexpr int NWV = TBM / 32;                            // waves
+  static constexpr int NT = 64 * NWV;                             // threads
+  static constexpr int NSTAGE = TBM == 256 ? 3 : 2;
+  static constexpr int STAGE = (TBM + BN) * BK * 2;               // bytes per LDS stage (A then B)
+  static constexpr int LDS = NSTAGE * STAGE > TBM * CROW * 2 ? NSTAGE * STAGE : TBM * CROW * 2;
+  static constexpr int ADMA = TBM / 8 / NWV;                      // A DMA instructions per wave per step: 4
+  static constexpr int BBLK = BN / 8;                             // 8-row B blocks per step: 20
+  static constexpr int BDMA = (BBLK + NWV - 1) / NWV;             // B DMA slots per wave: 5 | 3
+};
+constexpr int G_STAGE = GCfg<128>::STAGE;
+constexpr int G_LDS = GCfg<128>::LDS;
+constexpr int G_ADMA = GCfg<128>::ADMA;
+constexpr int G_BDMA = GCfg<128>::BDMA;
 
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// LDS-DMA destination (a non-template helper: the address-space cast of a TBM-dependent expression
+// inside the kernel template makes hipcc's host pass silently drop the kernel's launch stub)
+__device__ __forceinline__ __attribute__((address_space(3))) void* to_lds(const char* p) {
+  return (__attribute__((address_space(3))) void*)(p);
+}
 
 // erf for the GEGLU epilogue, branch-free: Abramowitz & Stegun 7.1.28,
 //   erf(|x|) = 1 - (1 + a1|x| + ... + a6|x|^6)^-16   (|error| <= 3e-7; <= 1.8e-6 in fp32 arithmetic),
@@ -103,18 +124,21 @@ __device__ __forceinline__ float erf_fast(float x) {
 // the fly (per row: the source pixel's offset and the output pixel's parities; a tap's source row /
 // column step is -1, 0 or +1 by parity, two selects + adds per row and step); 0 = 64-bit pointers
 // rebuilt per step (inputs beyond 2^31 bytes).
-template <int KS, int EPI = 0, int AM = 1>
-__global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) {
+template <int KS, int EPI, int AM, int TBM>
+__device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
+  using Cfg = GCfg<TBM>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
+  // B blocks of this wave: 8 * (w + Cfg::NWV * i) for i < nbd (8 waves: waves 0-3 take three, 4-7 two)
+  const int nbd = (Cfg::BBLK - w + Cfg::NWV - 1) / Cfg::NWV;
   const int M = a.batch * a.out_h * a.out_w;
   const int ntn = a.cout / BN;
   const int ks_n = EPI == 2 ? a.ksplit : 1;
   const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid0 % ks_n, bid = bid0 / ks_n;
   const int mt = bid / ntn, nt = bid - mt * ntn;
-  const int m0 = mt * GBM, n0 = nt * BN;
+  const int m0 = mt * TBM, n0 = nt * BN;
   const bf16* x = static_cast<const bf16*>(a.x);
   const bf16* wt = static_cast<const bf16*>(a.w);
   const int Kw = KS * KS * a.cin;
@@ -122,11 +146,11 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
 
   // this lane's rows: A instruction i of wave w covers rows 8*(w + 4i) .. +7, lane row l / 8
   const int lr = l >> 3, lj = l & 7;
-  int a_n[G_ADMA], a_iy[G_ADMA], a_ix[G_ADMA], a_c[G_ADMA];
-  bool a_ok[G_ADMA];
+  int a_n[Cfg::ADMA], a_iy[Cfg::ADMA], a_ix[Cfg::ADMA], a_c[Cfg::ADMA];
+  bool a_ok[Cfg::ADMA];
 #pragma unroll
-  for (int i = 0; i < G_ADMA; ++i) {
-    const int r = 8 * (w + NW * i) + lr;
+  for (int i = 0; i < Cfg::ADMA; ++i) {
+    const int r = 8 * (w + Cfg::NWV * i) + lr;
     const int p = m0 + r;
     a_ok[i] = p < M;
     const int pp = a_ok[i] ? p : 0;
@@ -137,12 +161,12 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
     a_ix[i] = ox * a.stride - a.pad;
     a_c[i] = swz(r, lj) * 8;                                  // source channel offset of this lane
   }
-  int b_c[G_BDMA];
+  int b_c[Cfg::BDMA];
 #pragma unroll
-  for (int i = 0; i < G_BDMA; ++i) b_c[i] = swz(8 * (w + NW * i) + lr, lj) * 8;
+  for (int i = 0; i < Cfg::BDMA; ++i) b_c[i] = swz(8 * (w + Cfg::NWV * i) + lr, lj) * 8;   // swz: (r >> 1) & 7 only
   // buffer forms: byte offsets at tap (0, 0) (AM 2: of the source pixel under the output pixel) and
   // the out-of-image tap masks (bit kh * KS + kw; AM 2: the output pixel's parities in bits 16, 17)
-  uint32_t a_off[G_ADMA], a_bad[G_ADMA], b_off[G_BDMA];
+  uint32_t a_off[Cfg::ADMA], a_bad[Cfg::ADMA], b_off[Cfg::BDMA];
   __amdgpu_buffer_rsrc_t xr, wr;
   const int sh = a.in_h >> (AM == 2), sw = a.in_w >> (AM == 2);   // stored image
   const int cin1 = a.cin - a.cin2;       // channels (and row stride) of x; x2 holds the last cin2
@@ -151,7 +175,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
                                            (uint32_t)a.batch * sh * sw * cin1 * 2u, 0x00020000);
     wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, (uint32_t)a.cout * Kw * 2u, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < G_ADMA; ++i) {
+    for (int i = 0; i < Cfg::ADMA; ++i) {
       if constexpr (AM == 2) {
         const int oy = a_iy[i] + a.pad, ox = a_ix[i] + a.pad;       // stride 1
         a_off[i] = (uint32_t)((((a_n[i] * sh + (oy >> 1)) * sw + (ox >> 1)) * a.cin + a_c[i]) * 2);
@@ -170,21 +194,21 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
       a_bad[i] = bad;
     }
 #pragma unroll
-    for (int i = 0; i < G_BDMA; ++i) {
-      const int row = 8 * (w + NW * i) + lr;
+    for (int i = 0; i < Cfg::BDMA; ++i) {
+      const int row = 8 * (w + Cfg::NWV * i) + lr < BN ? 8 * (w + Cfg::NWV * i) + lr : BN - 1;
       b_off[i] = (uint32_t)(((n0 + row) * Kw + b_c[i]) * 2);
     }
   }
 
   // two-source 1x1 input: the pixel's offsets in x2 (row stride cin2) for the K-steps past cin1
-  uint32_t a_off2[G_ADMA];
+  uint32_t a_off2[Cfg::ADMA];
   __amdgpu_buffer_rsrc_t xr2 = xr;
   if constexpr (AM == 1 && KS == 1) {
     if (a.x2) {
       xr2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x2), 0,
                                               (uint32_t)a.batch * a.in_h * a.in_w * a.cin2 * 2u, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < G_ADMA; ++i)
+      for (int i = 0; i < Cfg::ADMA; ++i)
         a_off2[i] = (uint32_t)((((a_n[i] * a.in_h + a_iy[i]) * a.in_w + a_ix[i]) * a.cin2 + a_c[i]) * 2);
     }
   }
@@ -194,8 +218,8 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
   auto dma = [&](int step, int stage) {
     const int tap = step / csteps, c0 = (step - tap * csteps) * BK;
     const int kh = tap / KS, kw = tap - kh * KS;
-    char* As = smem + stage * G_STAGE;
-    char* Bs = As + GBM * BK * 2;
+    char* As = smem + stage * Cfg::STAGE;
+    char* Bs = As + TBM * BK * 2;
     if constexpr (AM != 0) {
       if constexpr (AM == 2) {
         // source row step of tap row kh for output-row parity py: kh 0 -> py - 1, 1 -> 0, 2 -> py
@@ -204,33 +228,34 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
         const uint32_t cx0 = kw == 0 ? 0u - cs : 0u, cx1 = kw == 2 ? cs : 0u;
         const uint32_t xs = (uint32_t)(c0 * 2);
 #pragma unroll
-        for (int i = 0; i < G_ADMA; ++i) {
+        for (int i = 0; i < Cfg::ADMA; ++i) {
           const uint32_t o = a_off[i] + xs + ((a_bad[i] >> 16) & 1 ? ry1 : ry0) + ((a_bad[i] >> 17) & 1 ? cx1 : cx0);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(As + 8 * (w + Cfg::NWV * i) * BK * 2),
                                                    16, o | ((a_bad[i] >> tap) << 31), 0, 0, 0);
         }
       } else if (KS == 1 && a.x2 && c0 >= cin1) {           // 1x1, second source (wave-uniform)
         const uint32_t xs = (uint32_t)((c0 - cin1) * 2);
 #pragma unroll
-        for (int i = 0; i < G_ADMA; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr2, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
+        for (int i = 0; i < Cfg::ADMA; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr2, to_lds(As + 8 * (w + Cfg::NWV * i) * BK * 2),
                                                    16, (a_off2[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
       } else {
         const uint32_t xs = (uint32_t)(((kh * a.in_w + kw) * cin1 + c0) * 2);
 #pragma unroll
-        for (int i = 0; i < G_ADMA; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
+        for (int i = 0; i < Cfg::ADMA; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(As + 8 * (w + Cfg::NWV * i) * BK * 2),
                                                    16, (a_off[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
       }
       const uint32_t ws = (uint32_t)((tap * a.cin + c0) * 2);
 #pragma unroll
-      for (int i = 0; i < G_BDMA; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)(Bs + 8 * (w + NW * i) * BK * 2),
-                                                 16, b_off[i] + ws, 0, 0, 0);
+      for (int i = 0; i < Cfg::BDMA; ++i)
+        if (Cfg::BDMA * Cfg::NWV == Cfg::BBLK || i < nbd)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, to_lds(Bs + 8 * (w + Cfg::NWV * i) * BK * 2),
+                                                   16, b_off[i] + ws, 0, 0, 0);
       return;
     }
 #pragma unroll
-    for (int i = 0; i < G_ADMA; ++i) {
+    for (int i = 0; i < Cfg::ADMA; ++i) {
       const int iy = a_iy[i] + kh, ix = a_ix[i] + kw;
       const bool ok = a_ok[i] && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
       // upsample = 1: the input is nearest-upsampled x2 on the fly (Upsample3D, resnet.py:79-99):
@@ -239,15 +264,16 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
       const bf16* src = ok ? x + (((int64_t)a_n[i] * (a.in_h >> up) + (iy >> up)) * (a.in_w >> up) + (ix >> up)) *
                                      a.cin + c0 + a_c[i]
                            : zero;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + 8 * (w + NW * i) * BK * 2),
+      __builtin_amdgcn_global_load_lds(src, to_lds(As + 8 * (w + Cfg::NWV * i) * BK * 2),
                                        16, 0, 0);
     }
     const int64_t kofs = (int64_t)tap * a.cin + c0;
 #pragma unroll
-    for (int i = 0; i < G_BDMA; ++i) {
-      const int row = 8 * (w + NW * i) + lr;
+    for (int i = 0; i < Cfg::BDMA; ++i) {
+      if (Cfg::BDMA * Cfg::NWV != Cfg::BBLK && i >= nbd) continue;
+      const int row = 8 * (w + Cfg::NWV * i) + lr;
       const bf16* src = wt + (int64_t)(n0 + row) * Kw + kofs + b_c[i];
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + 8 * (w + NW * i) * BK * 2),
+      __builtin_amdgcn_global_load_lds(src, to_lds(Bs + 8 * (w + Cfg::NWV * i) * BK * 2),
                                        16, 0, 0);
     }
   };
@@ -260,11 +286,32 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
 
   const int fr = l & 15, fq = l >> 4;           // fragment row / 16-byte chunk within the 32-wide k-step
   dma(s_begin, 0);
+  if constexpr (Cfg::NSTAGE == 3)
+    if (s_begin + 1 < s_end) dma(s_begin + 1, 1);
+  int cur = 0;                                    // LDS stage of this step
   for (int step = s_begin; step < s_end; ++step) {
-    __syncthreads();                              // vmcnt(0): step's DMA landed; step-1's reads done
-    if (step + 1 < s_end) dma(step + 1, (step - s_begin + 1) & 1);
-    const char* As = smem + ((step - s_begin) & 1) * G_STAGE;
-    const char* Bs = As + GBM * BK * 2;
+    if constexpr (Cfg::NSTAGE == 2) {
+      __syncthreads();                            // vmcnt(0): step's DMA landed; step-1's reads done
+      if (step + 1 < s_end) dma(step + 1, cur ^ 1);
+    } else {
+      // this wave's DMA of `step` landed (the one of step + 1 may stay in flight: in-order vmcnt),
+      // then every wave's: the barrier also orders all reads of stage (step - 1) % 3 before the
+      // DMA of step + 2 overwrites it.  A raw s_barrier: __syncthreads() would drain the ring.
+      if (step + 1 < s_end) {
+        if (w < Cfg::BBLK % Cfg::NWV || Cfg::BBLK % Cfg::NWV == 0)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::ADMA + Cfg::BDMA) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::ADMA + Cfg::BDMA - 1) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (step + 2 < s_end) dma(step + 2, cur == 0 ? 2 : cur - 1);
+    }
+    const char* As = smem + cur * Cfg::STAGE;
+    const char* Bs = As + TBM * BK * 2;
+    cur = cur + 1 == Cfg::NSTAGE ? 0 : cur + 1;
 #pragma unroll
     for (int ks = 0; ks < BK / 8; ks += 4) {      // chunk index of the k-step (0 or 4)
       bf16x8 af[WTM], bfr[WTN];
@@ -320,7 +367,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
 #pragma clang fp contract(off)
     constexpr float kAlpha = 0.70710678118654752440f;
     const int half = a.cout / 2;
-    for (int c = tid; c < GBM * (BN / 16); c += 256) {
+    for (int c = tid; c < TBM * (BN / 16); c += Cfg::NT) {
       const int row = c / (BN / 16), ch = c - row * (BN / 16);
       const int p = m0 + row;
       if (p >= M) continue;
@@ -337,7 +384,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
     }
     return;
   }
-  for (int c = tid; c < GBM * (BN / 8); c += 256) {
+  for (int c = tid; c < TBM * (BN / 8); c += Cfg::NT) {
     const int row = c / (BN / 8), ch = c - row * (BN / 8);
     const int p = m0 + row;
     if (p >= M) continue;
@@ -351,6 +398,24 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) 
     *reinterpret_cast<bf16x8*>(y + o) = v;
   }
 }
+
+template <int KS, int EPI = 0, int AM = 1>
+__global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) {
+  conv_tile<KS, EPI, AM, 128>(a);
+}
+
+template <int KS, int EPI = 0, int AM = 1>
+__global__ __launch_bounds__(512, 1) void conv_kernel_b(const vp2p_conv_args a) {
+  conv_tile<KS, EPI, AM, 256>(a);
+}
+
+template <int KS, int EPI, int AM, int TBM> struct ConvKernel;
+template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 128> {
+  static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, AM>); }
+};
+template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 256> {
+  static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_b<KS, EPI, AM>); }
+};
 
 // split-K second pass: y = round(round(sum_s ws[s] + bias) + residual), the one-pass roundings
 __global__ __launch_bounds__(256) void conv_splitk_reduce(const vp2p_conv_args a) {
@@ -382,21 +447,48 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const vp2p_conv_args a
   *reinterpret_cast<bf16x8*>(static_cast<bf16*>(a.y) + o) = out;
 }
 
-template <int KS, int EPI, int AM>
+template <int KS, int EPI, int AM, int TBM>
 static int launch_g1(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, AM>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS) == hipSuccess;
+  using Cfg = GCfg<TBM>;
+  static const bool attr = hipFuncSetAttribute(ConvKernel<KS, EPI, AM, TBM>::fn(),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  hipLaunchKernelGGL((conv_kernel_g<KS, EPI, AM>), grid, dim3(256), G_LDS, s, a);
+  if constexpr (TBM == 128)
+    hipLaunchKernelGGL((conv_kernel_g<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
+  else
+    hipLaunchKernelGGL((conv_kernel_b<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
 // am: addressing form (see conv_kernel_g); the upsampling form exists for the 3x3 one-pass kernel only
-template <int KS, int EPI>
+template <int KS, int EPI, int TBM = 128>
 static int launch_g(const vp2p_conv_args& a, dim3 grid, int am, hipStream_t s) {
   if constexpr (KS == 3 && EPI == 0)
-    if (am == 2) return launch_g1<KS, EPI, 2>(a, grid, s);
-  return am == 1 ? launch_g1<KS, EPI, 1>(a, grid, s) : launch_g1<KS, EPI, 0>(a, grid, s);
+    if (am == 2) return launch_g1<KS, EPI, 2, TBM>(a, grid, s);
+  return am == 1 ? launch_g1<KS, EPI, 1, TBM>(a, grid, s) : launch_g1<KS, EPI, 0, TBM>(a, grid, s);
+}
+
+// The 256-row tile for one-pass launches that still fill the chip with one workgroup per CU.
+// Measured (profiles/r03_k10_tile_ab.jsonl, bit-equal outputs): it wins only on the long-K 1x1
+// GEMMs (M 131072, K 1280, N 320: 185.5 -> 170.2 us) and loses 2-8 % on the 3x3 convs and the
+// K = 320 GEMM / GEGLU shapes, whose per-tile prologue and epilogue no longer overlap a second
+// workgroup on the CU.  auto = 1x1 with K >= 1280 only.
+// VP2P_CONV_TILE=128 | 256 | auto (default) -- an A/B switch, read once.
+static int big_tile_mode() {
+  static const int m = [] {
+    const char* e = getenv("VP2P_CONV_TILE");
+    if (e && e[0] == '1') return 0;
+    if (e && e[0] == '2') return 2;
+    return 1;
+  }();
+  return m;
+}
+
+static bool use_big_tile(const vp2p_conv_args* a, int64_t M) {
+  const int mode = big_tile_mode();
+  if (mode == 0) return false;
+  const int64_t tiles = (M + 255) / 256 * (a->cout / BN);
+  return mode == 2 ? tiles >= 1 : (tiles >= 256 && a->kernel == 1 && a->cin >= 1280);
 }
 
 // K-split for this shape: 1 unless the grid would leave most CUs idle (the 8x8-latent convs)
@@ -473,6 +565,10 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
     if (rc != VP2P_OK) return rc;
     const int64_t n = M * (a->cout / 8);
     hipLaunchKernelGGL(conv::conv_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
+  } else if (conv::use_big_tile(a, M)) {
+    const dim3 gb((unsigned)((M + 255) / 256 * (a->cout / conv::BN)));
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 256>(*a, gb, fast, s);
+    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 256>(*a, gb, fast, s) : conv::launch_g<1, 0, 256>(*a, gb, fast, s);
   } else if (a->epilogue == VP2P_CONV_EPI_GEGLU) {
     rc = conv::launch_g<1, 1>(*a, grid, fast, s);
   } else {

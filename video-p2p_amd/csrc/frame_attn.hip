@@ -635,10 +635,14 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   }
 }
 
-static int k1_head_fastest() {   // VP2P_K1_GRID=bh: A/B switch to the (b, head)-major grid, read once
+// VP2P_K1_GRID=hf: A/B switch to the head-fastest grid, read once.  The default (b, head)-major grid
+// keeps all query blocks of one (b, head) on one XCD (its frame-0 K/V fetched into one L2): at the
+// res-64 launch FETCH x2 + WRITE = 427 MB vs 778 MB head-fastest (8 heads' K/V, 5.2 MB, thrash the
+// 4 MB L2), same time (0.868 vs 0.872 ms; profiles/r03_k1_grid_ab.txt)
+static int k1_head_fastest() {
   static const int hf = [] {
     const char* e = getenv("VP2P_K1_GRID");
-    return (e && e[0] == 'b') ? 0 : 1;
+    return (e && e[0] == 'h') ? 1 : 0;
   }();
   return hf;
 }
