@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", "--no-k1-events", dest="no_events", action="store_true",
                     help="do not bracket the attention launches with HIP events")
+    ap.add_argument("--graphs", type=int, default=0,
+                    help="1: replay each denoising step as a captured HIP graph (one process only; bit-equal)")
     ap.add_argument("--extras", default="auto", choices=["auto", "none", "all"],
                     help="secondary lines: inversion + fp32 edit (N = 1), clip-parallel (N > 1); auto = those")
     ap.add_argument("--mode", default="edit", choices=["edit", "nulltext", "k1long", "selftest"],
@@ -365,7 +367,10 @@ def nulltext_main(args, world, rank, dev):
     """configs[3] of BASELINE.json: NullInversion.invert (run_videop2p.py:614-624) of an 8-frame 512^2
     clip: 50 DDIM-inversion steps, then per step one conditional forward, up to --inner-steps
     forward+backward Adam iterations (random weights never reach the early-stop epsilon, so always
-    the maximum, the reference's worst case) and one guided step (B=2).  Clip-parallel over ranks."""
+    the maximum, the reference's worst case) and one guided step (B=2).  Over ranks: ``--shard frames``
+    (default) shards ONE clip's frames -- forward and backward exchanges, the embedding gradient
+    averaged before every Adam step (frame_parallel) -- ``--shard clips`` runs a clip per rank."""
+    from vp2p.frame_parallel import FrameShard, frame_parallel
     from vp2p.pipeline import NullInversion, VideoP2PPipeline
     from vp2p.unet3d import UNet3DConditionModel, init_random_
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -373,11 +378,17 @@ def nulltext_main(args, world, rank, dev):
     unet.eval()
     g = torch.Generator().manual_seed(1)
     ctx = torch.randn(2, 77, 768, generator=g).to(dev)
-    x0 = torch.randn(1, 4, args.frames, 64, 64, generator=torch.Generator().manual_seed(2 + rank)).to(dev)
+    frames_mode = args.shard == "frames" and world > 1
+    shard = FrameShard() if frames_mode else None
+    x0 = torch.randn(1, 4, args.frames, 64, 64,
+                     generator=torch.Generator().manual_seed(2 + (0 if frames_mode else rank))).to(dev)
+    if shard is not None:
+        x0 = shard.local(x0, 2)
 
     def run(steps):
-        inv = NullInversion(VideoP2PPipeline(unet), num_ddim_steps=steps)
-        return inv.invert(x0, "", num_inner_steps=args.inner_steps, text_embeddings=ctx)
+        with frame_parallel(shard):
+            inv = NullInversion(VideoP2PPipeline(unet), num_ddim_steps=steps)
+            return inv.invert(x0, "", num_inner_steps=args.inner_steps, text_embeddings=ctx)
 
     for _ in range(args.warmup):
         run(2)
@@ -391,15 +402,17 @@ def nulltext_main(args, world, rank, dev):
     elapsed = _max_over_ranks(time.perf_counter() - t0, world, dev)
     result = {
         "metric": "null-text inverted frames/sec (DDIM inversion + null-text optimisation, 512^2)",
-        "value": round(args.frames * args.steps * world / elapsed, 5), "unit": "inverted frames/s",
+        "value": round(args.frames * args.steps * (1 if frames_mode else world) / elapsed, 5),
+        "unit": "inverted frames/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
+        "scaling": "strong" if frames_mode else "weak",
         "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (random-init SD-1.5-geometry UNet3D, random text embeddings, x_0~N(0,1))",
         "config": {"workload": f"official-mode NullInversion.invert, {args.frames} frames 512^2, "
                                f"{args.ddim_steps} DDIM steps x {args.inner_steps} Adam iterations (max)",
                    "frames": args.frames, "ddim_steps": args.ddim_steps, "inner_steps": args.inner_steps,
-                   "parallelism": f"clip-parallel x{world}"},
+                   "parallelism": f"frame-sharded x{world} (RCCL)" if frames_mode else f"clip-parallel x{world}"},
         "output_finite": bool(torch.isfinite(x_t).all().item()) and all(bool(torch.isfinite(u).all()) for u in unc),
     }
     if rank == 0:
@@ -490,13 +503,14 @@ class Edit:
         self.layout = layout
         self.x_T = layout.local(x_T, 2) if layout is not None else x_T
         self.pipe = VideoP2PPipeline(self.unet)
+        self.graphs = bool(getattr(args, "graphs", 0)) and layout is None
 
     def __call__(self):
         from vp2p.frame_parallel import frame_parallel
         self.ctrl.reset()
         with frame_parallel(self.layout):
             return self.pipe(self.prompts, self.x_T.shape[2], latents=self.x_T, controller=self.ctrl, fast=True,
-                             text_embeddings=self.emb, num_inference_steps=self.steps)
+                             text_embeddings=self.emb, num_inference_steps=self.steps, graphs=self.graphs)
 
 
 def _time_edits(edit, warmup, steps, world, dev, timer=None):
@@ -542,6 +556,8 @@ def inversion_line(edit, dev, reps=2):
 
 def main():
     args = parse()
+    if args.graphs:
+        args.no_events = True          # replays bypass the Python launch wrappers the event timer hooks
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -1,7 +1,8 @@
 """Frame-sharded execution.
 
-CPU (gloo, world size 2): the exchange steps themselves -- frames<->tokens all-to-all, the cross-frame
-GroupNorm statistics, frame-0 broadcast, slicing and gathering -- against single-process results.
+CPU (gloo, world size 2 and 4): the exchange steps themselves -- frames<->tokens all-to-all, the
+frame-0 scatter + all-gather / broadcast, slicing and gathering -- against single-process results, and
+their adjoints (the frame-sharded backward) against single-process gradients.
 GPU (two ranks on the one MI355X, gloo with host staging): a frame-sharded UNet3D forward with the P2P
 controller equals the unsharded forward.
 """
@@ -45,15 +46,13 @@ def _cpu_worker(rank, world, port, out_path):
     tok = sh.to_tokens(loc.contiguous(), B)
     want = full.reshape(B, f, N, C)[:, :, rank * (N // world):(rank + 1) * (N // world)].reshape(-1, N // world, C)
     ok = [torch.equal(tok, want), torch.equal(sh.to_frames(tok, B), loc)]
-    # cross-frame GroupNorm statistics: sums over every rank's frames
-    x = torch.randn(2, f * 5, 4, 3, dtype=torch.float64).float()   # (B, f*HW, G, Cg), same on all ranks
-    xl = x.reshape(2, f, 5, 4, 3)[:, rank * (f // world):(rank + 1) * (f // world)].reshape(2, -1, 4, 3)
-    mean, var = sh.group_norm_stats(xl, xl.shape[1] * 3)
-    v_ref, m_ref = torch.var_mean(x, dim=(1, 3), unbiased=False)
-    ok += [torch.allclose(mean, m_ref, atol=1e-6), torch.allclose(var, v_ref, atol=1e-5)]
     t = torch.full((4,), float(rank))
     sh.broadcast_(t)
     ok.append(bool((t == 0).all()))
+    # the frame-0 exchange (a scatter + all-gather from 4 ranks up, else a broadcast)
+    t = torch.arange(24, dtype=torch.float32) + 100 * rank
+    sh.broadcast_async(t).wait()
+    ok.append(torch.equal(t, torch.arange(24, dtype=torch.float32)))
     lat = torch.arange(2 * 3 * f * 2, dtype=torch.float32).reshape(2, 3, f, 2)
     ok.append(torch.equal(sh.gather(sh.local(lat, 2), 2), lat))
     flat = torch.arange(5, dtype=torch.float32) + 10 * rank
@@ -62,13 +61,62 @@ def _cpu_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_exchanges_gloo_world2(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_exchanges_gloo(tmp_path, world):
     port = _port()
     out = str(tmp_path / "res")
-    mp.spawn(_cpu_worker, args=(2, port, out), nprocs=2, join=True)
-    for r in range(2):
+    mp.spawn(_cpu_worker, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
         res = torch.load(out + f".{r}")
         assert all(res), res
+
+
+def _toy_clip_loss(x, w, f_total):
+    """A stand-in for the UNet's three cross-frame couplings on a '(b f) n c' clip x: every frame reads
+    frame 0 (FrameAttention's K/V), then each token mixes over all frames (attn_temp)."""
+    B = x.shape[0] // f_total
+    y = x.reshape(B, f_total, *x.shape[1:])
+    y = torch.tanh(y * y[:, :1])                                          # frame-0 coupling
+    z = y * torch.softmax(y.sum(-1, keepdim=True), dim=1)                 # mixing over frames
+    return (z * w).sum()
+
+
+def _grad_worker(rank, world, port, out_path):
+    """The differentiable exchanges (frame0_hidden, to_tokens / to_frames) give the sharded toy loss
+    the same input gradient as the unsharded one."""
+    dist = _init(rank, world, port)
+    from vp2p import frame_parallel as fp
+    torch.manual_seed(0)
+    B, f, N, C = 2, 4, 8, 3
+    x = torch.randn(B * f, N, C, dtype=torch.float64)
+    w = torch.randn(B, f, N, C, dtype=torch.float64)
+    sh = fp.FrameShard()
+    fl = f // world
+    xl = x.reshape(B, f, N, C)[:, rank * fl:(rank + 1) * fl].reshape(B * fl, N, C).clone().requires_grad_(True)
+    # sharded: frame 0 from rank 0; to tokens (all frames, this rank's token slice); back to frames
+    y = xl.reshape(B, fl, N, C)
+    x0 = fp.frame0_hidden(sh, y[:, 0].contiguous())
+    y = torch.tanh(y * x0[:, None])
+    t = fp.to_tokens(sh, y.reshape(B * fl, N, C), B).reshape(B, f, N // world, C)
+    z = t * torch.softmax(t.sum(-1, keepdim=True), dim=1)
+    z = fp.to_frames(sh, z.reshape(B * f, N // world, C), B).reshape(B, fl, N, C)
+    loss = (z * w[:, rank * fl:(rank + 1) * fl]).sum()
+    loss.backward()
+    ref_x = x.clone().requires_grad_(True)
+    _toy_clip_loss(ref_x, w, f).backward()
+    want = ref_x.grad.reshape(B, f, N, C)[:, rank * fl:(rank + 1) * fl].reshape(B * fl, N, C)
+    torch.save([torch.allclose(xl.grad, want, atol=1e-12, rtol=1e-9)], out_path + f".{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_backward_gloo(tmp_path, world):
+    """the backward mirrors the forward collectives (null-text optimisation sharded over
+    frames); gradients equal the single-rank ones."""
+    out = str(tmp_path / "grad")
+    mp.spawn(_grad_worker, args=(world, _port(), out), nprocs=world, join=True)
+    for r in range(world):
+        assert all(torch.load(out + f".{r}")), r
 
 
 # ------------------------------------------------------------------------------------------------
@@ -166,3 +214,61 @@ def test_cfg_split_edit_matches_single(tmp_path, world):
         got = torch.load(out + f".{r}")
         err = (got - ref).abs().max() / ref.abs().max()
         assert err < 1e-4, (r, float(err))
+
+
+# ------------------------------------------------------------------------------------------------
+def _nulltext_case(frames):
+    import numpy as np
+    import vp2p
+    from vp2p.unet3d import UNet3DConditionModel, init_random_
+    unet = init_random_(UNet3DConditionModel(**CFG), seed=0, std=0.05).cuda().to(memory_format=torch.channels_last)
+    vp2p.register_attention_control(type("M", (), {"unet": unet})(), None)
+    g = np.random.default_rng(11)
+    x0 = torch.from_numpy(g.standard_normal((1, 4, frames, 32, 32)).astype(np.float32)).cuda()
+    ctx = torch.from_numpy(g.standard_normal((2, 77, 64)).astype(np.float32)).cuda()
+    return unet, x0, ctx
+
+
+def _run_nulltext(unet, x0, ctx, steps, inner):
+    from vp2p.pipeline import NullInversion, VideoP2PPipeline
+    inv = NullInversion(VideoP2PPipeline(unet), num_ddim_steps=steps)
+    inv.init_prompt("", ctx)
+    lats = inv.ddim_loop(x0)
+    unc = inv.null_optimization(lats, inner, 1e-5)
+    return lats, unc, inv.losses
+
+
+def _nulltext_worker(rank, world, port, out_path, frames, steps, inner):
+    """Official mode (DDIM inversion + null-text optimisation, run_videop2p.py:557-612) with the clip's
+    frames sharded over the ranks: the backward runs through the sharded GroupNorms, frame-0 K/V and
+    attn_temp all-to-alls, and the embedding gradient is averaged before each Adam step."""
+    dist = _init(rank, world, port)
+    from vp2p.frame_parallel import FrameShard, frame_parallel
+    unet, x0, ctx = _nulltext_case(frames)
+    sh = FrameShard()
+    with frame_parallel(sh):
+        lats, unc, losses = _run_nulltext(unet, sh.local(x0, 2), ctx, steps, inner)
+        lats = [sh.gather(t, 2).cpu() for t in lats]
+    torch.save({"lats": lats, "unc": [u.cpu() for u in unc], "losses": losses}, out_path + f".{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_frame_sharded_nulltext_matches_single(tmp_path):
+    frames, steps, inner = 4, 2, 2
+    out = str(tmp_path / "nt")
+    mp.spawn(_nulltext_worker, args=(2, _port(), out, frames, steps, inner), nprocs=2, join=True)
+    sys.path.insert(0, os.path.join(ROOT, "video-p2p_amd"))
+    unet, x0, ctx = _nulltext_case(frames)
+    lats, unc, losses = _run_nulltext(unet, x0, ctx, steps, inner)
+    for r in range(2):
+        got = torch.load(out + f".{r}")
+        for a, b in zip(got["lats"], lats):
+            assert float((a - b.cpu()).abs().max() / b.abs().max()) < 1e-4
+        assert len(got["losses"]) == len(losses)
+        for a, b in zip(got["losses"], losses):
+            assert abs(a - b) <= 1e-3 * abs(b) + 1e-9, (got["losses"], losses)
+        diff = (torch.cat(got["unc"]) - torch.cat([u.cpu() for u in unc])).abs()
+        # Adam's sqrt(v) normalisation: near-zero-gradient elements move by a fraction of lr (1e-2)
+        assert float(diff.mean()) < 1e-3 and float(diff.max()) < 2.5e-2, (float(diff.mean()), float(diff.max()))

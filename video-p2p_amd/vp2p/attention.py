@@ -115,9 +115,11 @@ class FrameAttention(CrossAttention):
             prescaled = True
         C = q.shape[-1]
         if not prescaled:
-            if shard is not None and shard.world > 1:
-                raise NotImplementedError("backward through frame-sharded FrameAttention (run null-text clip-parallel)")
             x0 = x.view(B, f, *x.shape[1:])[:, 0]
+            if shard is not None and shard.world > 1:
+                # frames sharded under autograd (null-text): rank 0's frame-0 hidden state, with the
+                # adjoint (its gradient summed over the ranks that projected K|V from it)
+                x0 = frame_parallel.frame0_hidden(shard, x0)
             kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
                           None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
             out = autograd.SharedKVAttention.apply(q, kv, f, self.heads, self.scale)
@@ -222,7 +224,11 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
             raise NotImplementedError("backward through a P2P-controlled or '(b d) f c' temporal attention")
         sh = frame_parallel.active()
         if sh is not None and sh.world > 1:
-            raise NotImplementedError("backward through frame-sharded temporal attention (run null-text clip-parallel)")
+            # frames sharded under autograd: the all-to-all frames <-> tokens and its adjoint
+            Bq = x.shape[0] // video_length
+            qkv = frame_parallel.to_tokens(sh, qkv, Bq)
+            out = autograd.TemporalAttention.apply(qkv, video_length * sh.world, h, module.scale)
+            return to_out(frame_parallel.to_frames(sh, out, Bq))
         return to_out(autograd.TemporalAttention.apply(qkv, video_length, h, module.scale))
     shard = frame_parallel.active() if temporal_layout == "bf" else None
     if shard is not None:

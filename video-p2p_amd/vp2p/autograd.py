@@ -10,6 +10,11 @@ gets its backward as a HIP kernel too:
 * ``TemporalAttention``  K3 forward / K3b backward -- plain hooked attn_temp (attention.py:262-268)
 * ``GroupNormFn``        K7 / K7b,  ``LayerNormFn`` K8 / K8b,  ``GEGLUFn`` K9 / K9b
 
+Frame-sharded (``frame_parallel``): every cross-frame coupling has a differentiable exchange --
+``GroupNormFn`` gathers forward and backward statistics partials, FrameAttention's frame-0 hidden
+state and attn_temp's all-to-alls carry their adjoints (``frame_parallel.frame0_hidden`` /
+``to_tokens`` / ``to_frames``).
+
 Only input gradients exist: the reference optimises the embedding alone (its Adam holds
 ``[uncond_embeddings]``, run_videop2p.py:589), so weight gradients are never consumed; asking for
 one raises instead of returning a silent zero.
@@ -86,22 +91,27 @@ class TemporalAttention(torch.autograd.Function):
 
 
 class GroupNormFn(torch.autograd.Function):
-    """5-D GroupNorm (+ channel add, + SiLU) of a channels-last '(b f) c h w' tensor."""
+    """5-D GroupNorm (+ channel add, + SiLU) of a channels-last '(b f) c h w' tensor.  ``shard``: a
+    FrameShard holding the other frames -- the forward all-gathers the statistics partials, the
+    backward its (sum dy, sum dy x^) partials, so both passes see the whole clip's statistics."""
 
     @staticmethod
-    def forward(ctx, x, add, weight, bias, groups: int, eps: float, frames: int, silu: bool):
-        out, stats = ops.group_norm(x, groups, weight, bias, eps, frames, silu=silu, add=add, return_stats=True)
+    def forward(ctx, x, add, weight, bias, groups: int, eps: float, frames: int, silu: bool, shard=None):
+        shard = shard if (shard is not None and shard.world > 1) else None
+        out, stats = ops.group_norm(x, groups, weight, bias, eps, frames, silu=silu, add=add, return_stats=True,
+                                    shard=shard)
         ctx.save_for_backward(x, add, weight, bias, stats[0])
-        ctx.cfg = (groups, eps, frames, silu, stats[1])
+        ctx.cfg = (groups, eps, frames, silu, stats[1], shard)
         return out
 
     @staticmethod
     def backward(ctx, dy):
         _no_weight_grad(ctx, 1, 2, 3)
         x, add, weight, bias, partials = ctx.saved_tensors
-        groups, eps, frames, silu, nsets = ctx.cfg
-        dx = ops.group_norm_bwd(x, dy, (partials, nsets), groups, weight, bias, eps, frames, silu=silu, add=add)
-        return dx, None, None, None, None, None, None, None
+        groups, eps, frames, silu, nsets, shard = ctx.cfg
+        dx = ops.group_norm_bwd(x, dy, (partials, nsets), groups, weight, bias, eps, frames, silu=silu, add=add,
+                                shard=shard)
+        return dx, None, None, None, None, None, None, None, None
 
 
 class LayerNormFn(torch.autograd.Function):

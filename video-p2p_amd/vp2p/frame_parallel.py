@@ -11,14 +11,23 @@ a broadcast of the LocalBlend sum from the conditional rank once the blend is ac
 Each rank holds frames [rank*f/G, (rank+1)*f/G) of every batch row.  Only three couplings in the
 UNet cross frames, and each gets exactly one collective:
 
-=============================  ==========================================  ===============================
+=============================  ==========================================  =================================
 reference site                 coupling                                    collective
-=============================  ==========================================  ===============================
-attention.py:296-302           FrameAttention reads frame 0's K/V          broadcast of (B, N, 2C) from rank 0
-resnet.py:142,158; unet.py:206 5-D GroupNorm statistics over (c/G, f, h, w) all-reduce of (sum x, sum x^2)
+=============================  ==========================================  =================================
+attention.py:296-302           FrameAttention reads frame 0's K/V          frame 0's NORMED hidden state
+                                                                           (B, N, C) from rank 0: scatter +
+                                                                           all-gather (world >= 4) or
+                                                                           broadcast; every rank projects K|V
+resnet.py:142,158; unet.py:206 5-D GroupNorm statistics over (c/G, f, h, w) all-gather of the K7 per-chunk
+                                                                           (count, mean, M2) partials
 attention.py:262-268           attn_temp attends over all f frames         all-to-all frames <-> tokens,
                                                                            before and after the kernel
-=============================  ==========================================  ===============================
+=============================  ==========================================  =================================
+
+Backward (the null-text optimisation, run_videop2p.py:580-612, frame-sharded): each collective has
+its adjoint -- the frame-0 hidden state's gradient is summed onto rank 0 (all-reduce), the GroupNorm
+backward all-gathers its (sum dy, sum dy x^) partials the same way, the all-to-alls swap direction --
+and the embedding gradient is all-reduced before the (replicated) Adam step.
 
 Cross-attention, FF, convs, the P2P edit (source/edit pairs are on the same rank), LocalBlend
 (strictly per frame, SURVEY finding 6) and the DDIM step stay rank-local.  With the NCCL (RCCL)
@@ -67,6 +76,18 @@ class _Done:
         return True
 
 
+class _Both:
+    """wait() on two collective handles (issued in order on the group's stream)."""
+
+    def __init__(self, *works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+
 class FrameShard:
     def __init__(self, group=None):
         if not dist.is_initialized():
@@ -102,12 +123,26 @@ class FrameShard:
 
     def broadcast_async(self, t: torch.Tensor):
         """Start an in-place broadcast of ``t`` from group rank 0; returns a handle whose ``wait()``
-        orders the current stream after it (RCCL: the collective runs on its own stream, so work
-        enqueued before ``wait()`` overlaps it; gloo staging completes it immediately)."""
+        orders the current stream after it (RCCL: the collectives run on their own stream, so work
+        enqueued before ``wait()`` overlaps them; gloo staging completes it immediately).
+
+        With 4+ ranks it is a scatter of 1/G slices from rank 0 followed by an in-place all-gather:
+        on point-to-point xGMI the root then sends (G-1)/G of the bytes over G-1 links at once instead
+        of pushing every byte down one ring, and the all-gather's traffic is spread over all ranks."""
         if self.staged and t.is_cuda:
             self.broadcast_(t)
             return _Done()
-        return dist.broadcast(t, src=self.src0, group=self.group, async_op=True)
+        flat = t.view(-1)
+        if self.world < 4 or flat.numel() % self.world:
+            return dist.broadcast(t, src=self.src0, group=self.group, async_op=True)
+        n = flat.numel() // self.world
+        mine = flat[self.rank * n:(self.rank + 1) * n]
+        w1 = dist.scatter(mine, list(flat.split(n)) if self.rank == 0 else None, src=self.src0, group=self.group,
+                          async_op=True)
+        if self.staged:          # gloo runs async ops on worker threads, unordered: finish the scatter
+            w1.wait()
+        w2 = dist.all_gather_into_tensor(flat, mine, group=self.group, async_op=True)
+        return _Both(w1, w2)     # RCCL: both on the group's stream, in issue order
 
     def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
         if self.staged and inp.is_cuda:
@@ -161,14 +196,62 @@ class FrameShard:
         dist.all_gather_into_tensor(out, src.contiguous(), group=self.group)
         return out.to(t.device)
 
-    def group_norm_stats(self, xv: torch.Tensor, n_local: int):
-        """Global (mean, var) per (b, group) of xv (B, L, G, Cg) fp32 summed over dims (1, 3)."""
-        s = torch.stack([xv.sum(dim=(1, 3)), (xv * xv).sum(dim=(1, 3))])          # (2, B, G)
-        self.all_reduce_(s)
-        n = n_local * self.world
-        mean = s[0] / n
-        var = (s[1] / n - mean * mean).clamp_min_(0.0)
-        return mean, var
+
+# -- differentiable exchanges (the frame-sharded null-text backward) -----------------------------------
+class _Frame0Hidden(torch.autograd.Function):
+    """Forward: rank 0's tensor on every rank (frame 0's normed hidden state, attention.py:296-302).
+    Backward: the ranks' gradients summed onto rank 0 (every rank's K|V projection read it)."""
+
+    @staticmethod
+    def forward(ctx, x0, shard):
+        ctx.shard = shard
+        out = x0.detach().clone(memory_format=torch.contiguous_format) if shard.rank == 0 else \
+            torch.empty(x0.shape, device=x0.device, dtype=x0.dtype)
+        shard.broadcast_async(out).wait()
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous().clone()
+        ctx.shard.all_reduce_(g)
+        return (g if ctx.shard.rank == 0 else torch.zeros_like(g)), None
+
+
+class _ToTokens(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, shard, batch):
+        ctx.shard, ctx.batch = shard, batch
+        return shard.to_tokens(x.contiguous(), batch)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.shard.to_frames(g.contiguous(), ctx.batch), None, None
+
+
+class _ToFrames(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, shard, batch):
+        ctx.shard, ctx.batch = shard, batch
+        return shard.to_frames(y.contiguous(), batch)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.shard.to_tokens(g.contiguous(), ctx.batch), None, None
+
+
+def frame0_hidden(shard: FrameShard, x0: torch.Tensor) -> torch.Tensor:
+    """Rank 0's ``x0`` on every rank; differentiable (gradient all-reduced onto rank 0)."""
+    return _Frame0Hidden.apply(x0, shard)
+
+
+def to_tokens(shard: FrameShard, x: torch.Tensor, batch: int) -> torch.Tensor:
+    """Differentiable ``FrameShard.to_tokens`` (its adjoint is ``to_frames``)."""
+    return _ToTokens.apply(x, shard, batch)
+
+
+def to_frames(shard: FrameShard, y: torch.Tensor, batch: int) -> torch.Tensor:
+    """Differentiable ``FrameShard.to_frames`` (its adjoint is ``to_tokens``)."""
+    return _ToFrames.apply(y, shard, batch)
 
 
 def _staged_run(group, fn, t: torch.Tensor) -> torch.Tensor:

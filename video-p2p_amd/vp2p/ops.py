@@ -463,9 +463,10 @@ def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor],
 
 
 def group_norm_bwd(x: torch.Tensor, dy: torch.Tensor, stats, num_groups: int, weight, bias, eps: float,
-                   frames: int, silu: bool = False, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   frames: int, silu: bool = False, add: Optional[torch.Tensor] = None, shard=None) -> torch.Tensor:
     """Input gradient of ``group_norm`` (K7b) given the forward's ``stats`` = (partials, nsets);
-    dy and the result are channels-last like x."""
+    dy and the result are channels-last like x.  ``shard``: the FrameShard of the forward -- the
+    per-chunk backward partials of every rank are gathered before the apply kernel."""
     partials, nsets = stats
     if not dy.is_contiguous(memory_format=torch.channels_last):
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -480,7 +481,11 @@ def group_norm_bwd(x: torch.Tensor, dy: torch.Tensor, stats, num_groups: int, we
     dym = _rows_view(dy)
     check(lib.vp2p_group_norm_bwd_reduce(ctypes.byref(a), _ptr(partials), nsets, _ptr(dym), _ptr(bpart), s),
           "vp2p_group_norm_bwd_reduce")
-    check(lib.vp2p_group_norm_bwd_apply(ctypes.byref(a), _ptr(partials), nsets, _ptr(dym), _ptr(bpart), 1,
+    bsets = 1
+    if shard is not None and shard.world > 1:
+        bpart = shard.all_gather_flat(bpart)
+        bsets = shard.world
+    check(lib.vp2p_group_norm_bwd_apply(ctypes.byref(a), _ptr(partials), nsets, _ptr(dym), _ptr(bpart), bsets,
                                         _ptr(_rows_view(dx)), s), "vp2p_group_norm_bwd_apply")
     return dx
 

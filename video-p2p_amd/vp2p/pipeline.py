@@ -289,6 +289,8 @@ class NullInversion:
         embedding, so its weight gradients are never used)."""
         from . import autograd
         unet = self.model.unet
+        shard = frame_parallel.active()
+        shard = shard if (shard is not None and shard.world > 1) else None
         was = [p.requires_grad for p in unet.parameters()]
         unet.requires_grad_(False)
         try:
@@ -312,6 +314,15 @@ class NullInversion:
                                                        consts, GUIDANCE_SCALE)
                     opt.zero_grad()
                     loss.backward()
+                    if shard is not None:
+                        # frames sharded: the clip's loss is the mean of the ranks' equal-size MSEs, so
+                        # its embedding gradient is the mean of theirs (every rank then takes the same
+                        # Adam step) and the early-stop test reads the clip's loss
+                        red = torch.cat([uncond.grad.reshape(-1), loss.detach().reshape(1).to(uncond.grad.dtype)])
+                        shard.all_reduce_(red)
+                        red /= shard.world
+                        uncond.grad.copy_(red[:-1].view_as(uncond.grad))
+                        loss = red[-1]
                     opt.step()
                     loss_item = loss.item()
                     self.losses.append(loss_item)

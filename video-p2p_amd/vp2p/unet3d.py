@@ -55,9 +55,7 @@ def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bo
     w, b = (norm.weight, norm.bias) if norm.affine else (None, None)
     add = None if add is None else add.contiguous()
     if autograd.needs_grad(x, w, b, add):
-        if shard is not None and shard.world > 1:
-            raise NotImplementedError("backward through a frame-sharded GroupNorm (run null-text clip-parallel)")
-        return autograd.GroupNormFn.apply(x, add, w, b, norm.num_groups, norm.eps, frames, silu)
+        return autograd.GroupNormFn.apply(x, add, w, b, norm.num_groups, norm.eps, frames, silu, shard)
     return ops.group_norm(x, norm.num_groups, w, b, norm.eps, frames, silu=silu, add=add, shard=shard, x2=x2)
 
 
