@@ -352,9 +352,15 @@ struct CrossV3Cfg {
 // T77: the SD text context (77 tokens, KB = 3): in the last 32-key block only keys 64..76 are real,
 // so accumulator registers 8..15 (keys 80..95 for both lane halves) are never computed through exp
 // and the block's second PV k-step (keys 80..95) is skipped.
-template <int D, int KB, bool T77 = false>
+// MODE 0: Q fragments loaded straight from HBM one block ahead; 1: the same two blocks ahead;
+// 2 ("staged", needs tokens_q % 32 == 0): a wave moves its block's Q rows and O rows as whole
+// 2d-byte row segments (5 / 10 / 20 lanes per row for d = 40 / 80 / 160) through a private LDS
+// tile, instead of fragment-shaped loads / stores that touch 32 rows x 16-32 B per instruction.
+template <int D, int KB, bool T77 = false, int MODE = 0>
 __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(const vp2p_cross_attn_args a, int iters, int b0,
                                                                                int nx, int rows) {
+  constexpr int PF = MODE == 1 ? 2 : 1;
+  constexpr bool STG = MODE == 2;
   using T = bf16;
   using M = Mfma<T>;
   using C = CrossCfg<T, D>;
@@ -433,17 +439,75 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
 #pragma unroll
     for (int s = 0; s < C::KS; ++s) dst[s] = ok ? M::row_frag(row, s, h, D) : M::zero();
   };
-  bf16x8 qn[C::KS];
-  load_q(qi, fr, pos, qn);
-  int fr_n = fr, pos_n = pos;
+  // staged mode: this wave's LDS tile (32 rows x QROW, columns D..DP-1 zero) and its row-segment chunks
+  constexpr int QROW = C::DP + 8, CPR = D / 8, NCHK = (32 * CPR + 63) / 64;
+  T* Qs = reinterpret_cast<T*>(smem + V3::LDS + ((LBS * NKV * 4 + 15) & ~15)) + w * 32 * QROW;
+  u32x4 qraw[STG ? NCHK : 1];
+  auto load_raw = [&](int qi_, int f_, int p_) {        // the block of lane row r = qi_ (frame f_, token p_)
+    const int q0 = qi_ - r, n0 = p_ - r;                // tokens_q % 32 == 0: the block sits in frame f_
+#pragma unroll
+    for (int i = 0; i < NCHK; ++i) {
+      const int c = i * 64 + l, row = c / CPR, ch = c - row * CPR;
+      qraw[i] = (c < 32 * CPR && q0 + row < FQ)
+                    ? *reinterpret_cast<const u32x4*>(qbase + f_ * a.q_sf + (n0 + row) * a.q_sn + ch * 8)
+                    : u32x4{0, 0, 0, 0};
+    }
+  };
+  if constexpr (STG) {
+    if constexpr (C::DP > D)
+      for (int i = l; i < 32 * (C::DP - D); i += 64) {
+        const int row = i / (C::DP - D);
+        Qs[row * QROW + D + (i - row * (C::DP - D))] = (T)0.f;
+      }
+  }
+  bf16x8 qn[C::KS], qn2[C::KS];
+  if constexpr (STG) load_raw(qi, fr, pos);
+  else load_q(qi, fr, pos, qn);
+  int fr_n = fr, pos_n = pos;          // (frame, token) of block qi
+  int qi2 = qi, fr2 = fr, pos2 = pos;  // PF 2: of the block fetched two ahead
+  if constexpr (PF == 2) {
+    if (iters > 1) {
+      advance(fr2, pos2);
+      qi2 += step;
+      load_q(qi2, fr2, pos2, qn2);
+    }
+  }
 
   for (int it = 0; it < iters; ++it) {
     bf16x8 qf[C::KS];
+    if constexpr (STG) {
+      // this block's row segments -> LDS (the wave's own tile: LDS ops of one wave stay in order)
 #pragma unroll
-    for (int s = 0; s < C::KS; ++s) qf[s] = qn[s];
+      for (int i = 0; i < NCHK; ++i) {
+        const int c = i * 64 + l, row = c / CPR, ch = c - row * CPR;
+        if (c < 32 * CPR) *reinterpret_cast<u32x4*>(Qs + row * QROW + ch * 8) = qraw[i];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) qf[s] = qn[s];
+    }
     const int qcur = qi;
     const int fcur = fr_n, pcur = pos_n;
-    if (it + 1 < iters) {
+    if constexpr (STG) {
+      if (it + 1 < iters) {
+        advance(fr_n, pos_n);
+        qi += step;
+        load_raw(qi, fr_n, pos_n);
+      }
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qs + r * QROW + 16 * s + 8 * h);
+    } else if constexpr (PF == 2) {
+      if (it + 1 < iters) {
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) qn[s] = qn2[s];
+        qi = qi2, fr_n = fr2, pos_n = pos2;
+        if (it + 2 < iters) {
+          advance(fr2, pos2);
+          qi2 += step;
+          load_q(qi2, fr2, pos2, qn2);
+        }
+      }
+    } else if (it + 1 < iters) {
       advance(fr_n, pos_n);
       qi += step;
       load_q(qi, fr_n, pos_n, qn);
@@ -537,7 +601,7 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
           o = M::mma(*reinterpret_cast<const bf16x8*>(Vs + (32 * t + r) * V3::VROW + kb * 32 + 16 * sp + 8 * h), pf[kb][sp], o);
         }
       __builtin_amdgcn_sched_barrier(0);
-      if (qv) {
+      if (STG || qv) {
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
           const int dc = 32 * t + 8 * gq + 4 * h;
@@ -545,9 +609,21 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
             bf16x4 v;
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[4 * gq + j] * oscale);
-            *reinterpret_cast<bf16x4*>(orow + dc) = v;
+            if constexpr (STG) *reinterpret_cast<bf16x4*>(Qs + r * QROW + dc) = v;
+            else *reinterpret_cast<bf16x4*>(orow + dc) = v;
           }
         }
+      }
+    }
+    if constexpr (STG) {     // the block's O rows out of the LDS tile as whole row segments
+      const int q0 = qcur - r, n0 = pcur - r;
+      T* ob = obase + fcur * a.o_sf;
+#pragma unroll
+      for (int i = 0; i < NCHK; ++i) {
+        const int c = i * 64 + l, row = c / CPR, ch = c - row * CPR;
+        if (c < 32 * CPR && q0 + row < FQ)
+          *reinterpret_cast<u32x4*>(ob + (n0 + row) * a.o_sn + ch * 8) =
+              *reinterpret_cast<const u32x4*>(Qs + row * QROW + ch * 8);
       }
     }
   }
@@ -847,6 +923,28 @@ static int cross_edit_kernel() {
   return k;
 }
 
+// VP2P_K2_WGCU=n: v3 grid target of n workgroups per CU (default 4) -- an A/B switch, read once
+// (measured no faster at 6, 8, 12; nor two Q blocks ahead: profiles/r03_k2_v3_pf_wgcu_ab.jsonl)
+static int cross_v3_wgcu() {
+  static const int n = [] {
+    const char* e = getenv("VP2P_K2_WGCU");
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 && v <= 64 ? v : 4;
+  }();
+  return n;
+}
+// v3's Q/O path (cross_attn_kernel_v3 MODE): staged rows (2) for d <= 80 -- res-64 non-edit launch
+// 53.8 -> 48.5 us, res-32 edit launch 56.5 -> 53.4 us, bit-equal (profiles/r03_k2_v3_staged_ab.jsonl)
+// -- and fragment loads (0) for d = 160, where the 20-lane rows cost occupancy (31.0 -> 36.4 us).
+// VP2P_K2_V3=0|1|2 forces a mode (A/B), read once.
+static int cross_v3_mode(int d) {
+  static const int n = [] {
+    const char* e = getenv("VP2P_K2_V3");
+    return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
+  }();
+  return n >= 0 ? n : (d <= 80 ? 2 : 0);
+}
+
 // VP2P_K2_GRID=3d: A/B switch back to v3's (x, row, head) grid (default: 1-D, XCD-grouped), read once
 static bool cross_grid_1d() {
   static const bool g = [] {
@@ -866,25 +964,41 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
     const int64_t qblocks = (FQ + 31) / 32;
     const int64_t per_wg = (qblocks + 3) / 4;                   // iterations of one stream, all blocks
     const int64_t gh = (int64_t)rows * a->heads;
-    // ~4 workgroups per CU over the (row, head) grid; each stream then loops `iters` blocks
-    int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (1024 + gh - 1) / gh));
+    // ~cross_v3_wgcu() workgroups per CU over the (row, head) grid; each stream then loops `iters` blocks
+    const int64_t target = 256 * cross_v3_wgcu();
+    int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (target + gh - 1) / gh));
     const int iters = (int)((per_wg + nx - 1) / nx);
     nx = (per_wg + iters - 1) / iters;
     if (rows > 65535 || a->heads > 65535 || nx > 0x7fffffff) return VP2P_E_SHAPE;
     const int sets = a->lb_sets == 2 ? 2 : 1;
-    const size_t lds = (size_t)V3::LDS + (size_t)sets * a->tokens_kv * sizeof(float);
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    static const bool attr77 = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true>),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    if (!attr || !attr77 || lds > 160 * 1024) return VP2P_E_LAUNCH;
+    const bool t77 = KB == 3 && a->tokens_kv == 77;
+    int mode = cross_v3_mode(D);
+    if (mode == 2 && a->tokens_q % 32) mode = 0;             // staged rows need whole blocks per frame
+    size_t lds = (size_t)V3::LDS + (size_t)sets * a->tokens_kv * sizeof(float);
+    if (mode == 2) lds = ((lds + 15) & ~(size_t)15) + (size_t)4 * 32 * (CrossCfg<bf16, D>::DP + 8) * 2;
+    const void* fn = nullptr;
+    switch (mode * 2 + (t77 ? 1 : 0)) {
+      case 0: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, false, 0>); break;
+      case 1: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true, 0>); break;
+      case 2: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, false, 1>); break;
+      case 3: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true, 1>); break;
+      case 4: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, false, 2>); break;
+      default: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true, 2>); break;
+    }
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+        lds > 160 * 1024)
+      return VP2P_E_LAUNCH;
     const bool g1 = cross_grid_1d() && nx * rows * a->heads <= 0x7fffffff;
     const dim3 grid = g1 ? dim3((unsigned)(nx * rows * a->heads)) : dim3((unsigned)nx, (unsigned)rows, (unsigned)a->heads);
     const int nx1 = g1 ? (int)nx : 0;
-    if (KB == 3 && a->tokens_kv == 77)
-      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows);
-    else
-      hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows);
+    switch (mode * 2 + (t77 ? 1 : 0)) {
+      case 0: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, false, 0>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
+      case 1: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true, 0>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
+      case 2: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, false, 1>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
+      case 3: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true, 1>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
+      case 4: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, false, 2>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
+      default: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true, 2>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
+    }
     return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
   };
   // v3e over the edited conditional half (prompts = 2, bf16); returns VP2P_E_SHAPE to fall back to v1
