@@ -203,7 +203,9 @@ def _edit_fixture(name):
 
 # End-to-end bars: fp32 -- final-latent PSNR >= 100 dB and K6's applied LocalBlend masks
 # equal to the reference's (at most 1 flip per 10^4 pixels); bf16 -- final-latent PSNR >= 45 dB.  Every
-# saved reference mask is non-trivial (true fraction in [0.05, 0.95], asserted by the generator and here).
+# saved reference mask is non-trivial (true fraction in [0.05, 0.95], asserted by the generator and here;
+# the blend maps are summed over steps, so late masks that widen past 0.95 are not saved, only their
+# fraction -- the first blend step's mask always is).
 # The fp32 rabbit8 case runs 50 fp32 UNet steps (~145 s, profiles/r02_edit_pipeline_durations.log),
 # more than a 120 s per-test limit on the command line allows.
 @pytest.mark.timeout(600)
