@@ -10,11 +10,15 @@ CLIP (seed 1; CLIP and VAE are excluded from the metric), x_T ~ N(0, 1) (seed 2)
 
 Multi-GPU: ``python bench.py --gpus N`` starts N rank processes itself (a torchrun child, launched
 before this process touches the GPU); under an external torchrun it reads RANK / WORLD_SIZE.  The
-default ``--shard frames`` runs ONE clip over all ranks (strong scaling, frame_parallel.EditLayout):
-the CFG halves on two rank groups, the frames sharded inside each half, RCCL carrying the frame-0
-hidden-state broadcast, the 5-D GroupNorm statistics and the attn_temp all-to-all.  value = frames
-/ max-over-ranks wall time.  ``--shard clips``: every rank edits its own clip (weak scaling); it is
-also reported as the secondary ``clip_parallel`` field of a frame-sharded run.
+default ``--shard frames`` runs ONE clip over all ranks (frame_parallel.EditLayout): the CFG halves
+on two rank groups, the frames sharded inside each half, RCCL carrying the frame-0 hidden-state
+scatter + all-gather, the 5-D GroupNorm statistics and the attn_temp all-to-all.  ``--scale weak``
+(default): the clip has 8 x N frames, so every rank keeps the N = 1 edit's per-forward work (32
+images) -- frame-sharded weak scaling, the north star's "frames sharded across 1-8 GPUs" at the
+bench's per-GPU size; the 8-frame clip over the same N ranks (strong scaling: 2 frames per rank at
+N = 8, where the small per-launch work bounds it) is the secondary ``strong_scaling``
+field, ``--scale strong`` makes it the headline.  value = clip frames / max-over-ranks wall time.
+``--shard clips``: every rank edits its own clip, no collective; also reported as ``clip_parallel``.
 
 The JSON line carries, measured live with HIP events on the launch stream inside the timed region:
 ``roofline`` for K1 (frame attention, the dominant MFMA-bound kernel: its res-64 launches),
@@ -68,6 +72,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", "--no-k1-events", dest="no_events", action="store_true",
                     help="do not bracket the attention launches with HIP events")
+    ap.add_argument("--scale", default="weak", choices=["weak", "strong"],
+                    help="frame-sharded N > 1: weak = ONE clip of frames x N frames sharded over the N ranks "
+                         "(every rank keeps the N = 1 edit's 32 images per UNet forward); strong = the "
+                         "frames-frame clip itself (reported as the strong_scaling secondary either way)")
     ap.add_argument("--graphs", type=int, default=0,
                     help="1: replay each denoising step as a captured HIP graph (one process only; bit-equal)")
     ap.add_argument("--extras", default="auto", choices=["auto", "none", "all"],
@@ -598,6 +606,14 @@ def main():
     peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
     frames_mode = args.shard == "frames" and world > 1
     layout = None
+    f1 = args.frames                                    # the clip of the N = 1 workload (configs[1]: 8)
+    weak_frames = frames_mode and args.scale == "weak"
+    if weak_frames:
+        # weak frame scaling: one clip of f1 * N frames, sharded (CFG split x frame shards), so each
+        # rank runs the N = 1 edit's per-forward work (B2 x 2 f1 frames = B4 x f1 images) and every
+        # cross-frame exchange of the layout carries real traffic
+        args.frames = f1 * world
+    layout = None
     if frames_mode:
         from vp2p.frame_parallel import EditLayout
         layout = EditLayout()
@@ -614,7 +630,8 @@ def main():
         "unit": "edited frames/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
-        "higher_is_better": True, "scaling": "strong" if frames_mode else "weak", "vs_baseline": None,
+        "higher_is_better": True, "scaling": "strong" if (frames_mode and not weak_frames) else "weak",
+        "vs_baseline": None,
         "dtype": args.dtype, "data": "synthetic (random-init SD-1.5-geometry UNet3D, random text embeddings, x_T~N(0,1))",
         "config": {"workload": f"{edit.name} --fast: {edit.kind}, {f} frames 512^2, "
                                f"{args.ddim_steps}-step DDIM, UNet batch 4", "frames": f, "resolution": 512,
@@ -626,11 +643,24 @@ def main():
     }
     extras = args.extras != "none"
     with torch.no_grad():
+        if extras and world > 1 and frames_mode and weak_frames:
+            # secondary: strong frame scaling -- the N = 1 clip (f1 frames) sharded over the N ranks
+            del edit
+            torch.cuda.empty_cache()
+            s_args = argparse.Namespace(**{**vars(args), "frames": f1})
+            s_lay = EditLayout()
+            strong = Edit(s_args, dev, dtype, s_lay, seed_offset=0)
+            t_s, _ = _time_edits(strong, 1, 1, world, dev)
+            result["strong_scaling"] = {"value": round(f1 / t_s, 4), "ms_per_step": round(t_s * 1e3, 2),
+                                        "frames": f1, "scaling": "strong",
+                                        "parallelism": s_lay.describe() + " (RCCL)"}
+            del strong
         if extras and world > 1 and frames_mode:
-            # secondary: every rank edits its own full clip (no collective), one timed edit
-            clip = Edit(args, dev, dtype, None, seed_offset=rank)
+            # secondary: every rank edits its own N = 1 clip (no collective), one timed edit
+            c_args = argparse.Namespace(**{**vars(args), "frames": f1})
+            clip = Edit(c_args, dev, dtype, None, seed_offset=rank)
             t_clip, _ = _time_edits(clip, 1, 1, world, dev)
-            result["clip_parallel"] = {"value": round(f * world / t_clip, 4), "ms_per_step": round(t_clip * 1e3, 2),
+            result["clip_parallel"] = {"value": round(f1 * world / t_clip, 4), "ms_per_step": round(t_clip * 1e3, 2),
                                        "scaling": "weak", "parallelism": f"clip-parallel x{world}"}
             del clip
         if extras and world == 1:
