@@ -562,6 +562,25 @@ def inversion_line(edit, dev, reps=2):
             "output_finite": bool(torch.isfinite(x_t).all().item())}
 
 
+def vae_line(latents, dev, dtype, reps=2):
+    """VAE decode of the edit's output latents (TuneAVideoPipeline.decode_latents,
+    pipeline_tuneavideo.py:239-256: (b f) frames in batches of 4, vp2p.vae on K7 + MIOpen), outside
+    the headline metric (the reference's edit timing also stops at the latents)."""
+    from vp2p.vae import AutoencoderKL, decode_latents, init_vae_random_
+    vae = init_vae_random_(AutoencoderKL(), seed=0).to(dev, dtype).to(memory_format=torch.channels_last).eval()
+    video = decode_latents(vae, latents)                 # first use: MIOpen picks / loads its kernels
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        video = decode_latents(vae, latents)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    n = latents.shape[0] * latents.shape[2]
+    return {"metric": "decoded frames/sec (VAE decode of the edited latents, 512^2)", "value": round(n / dt, 3),
+            "unit": "decoded frames/s", "frames": n, "ms_per_clip": round(dt * 1e3, 1), "dtype": str(dtype).split(".")[-1],
+            "output_finite": bool(torch.isfinite(video).all().item())}
+
+
 def main():
     args = parse()
     if args.graphs:
@@ -665,6 +684,7 @@ def main():
             del clip
         if extras and world == 1:
             result["inversion"] = inversion_line(edit, dev)
+            result["vae_decode"] = vae_line(out, dev, dtype)
             if dtype == torch.bfloat16 and args.extras in ("auto", "all"):
                 del edit
                 torch.cuda.empty_cache()
