@@ -66,25 +66,36 @@ __device__ __forceinline__ f32x4v mfma16(bf16x8 a, bf16x8 b, f32x4v c) {
 __device__ __attribute__((aligned(16))) unsigned int kZero16[4] = {0, 0, 0, 0};
 
 constexpr int GBM = 128, NW = 4;                               // the split-K / small-M tile
-// TBM = 128: 4 waves (2 x 2 of 64 x 80), two LDS stages, one __syncthreads per K-step, two
-// workgroups per CU.  TBM = 256 ("big"): 8 waves (4 x 2 of 64 x 80), THREE LDS stages (3 x 52 KB),
-// one workgroup per CU; the DMA of steps s+1 and s+2 are in flight under step s's MFMAs (counted
-// vmcnt + raw s_barrier, so the barrier does not drain the ring).  Same per-output K order and
-// MFMA sequence: bit-equal results.
-template <int TBM> struct GCfg {
-  static constexpr int NWV = TBM / 32;                            // waves
+// Tile configurations of conv_tile (CF):
+//  0: 128 x 160, 4 waves (2 x 2 of 64 x 80), two LDS stages, one __syncthreads per K-step, two
+//     workgroups per CU -- the default;
+//  1: 256 x 160, 8 waves (4 x 2 of 64 x 80), THREE LDS stages (3 x 52 KB), one workgroup per CU;
+//     the DMA of steps s+1 and s+2 in flight under step s's MFMAs (counted vmcnt + raw s_barrier,
+//     so the barrier does not drain the ring) -- the long-K 1x1 GEMMs;
+//  2: 256 x 320 "wide", 8 waves (2 x 4 of 128 x 80: 8 x 5 MFMA tiles, every A fragment used 5x,
+//     every B fragment 8x), two stages (2 x 72 KB), one workgroup per CU: twice the MFMAs per LDS
+//     byte read and per barrier of 0 / 1 (Cout % 320 == 0; the epilogue runs in two 128-row passes).
+// All: the same per-output K order and MFMA sequence, so bit-equal results.
+template <int TBM_, int TBN_, int WTM_, int NST_> struct GTile {
+  static constexpr int TBM = TBM_, TBN = TBN_, WTM = WTM_, NSTAGE = NST_;
+  static constexpr int WR = 16 * WTM;                             // output rows per wave
+  static constexpr int WCOL = TBN / 80;                           // waves along N (80 columns each)
+  static constexpr int NWV = (TBM / WR) * WCOL;                   // waves
   static constexpr int NT = 64 * NWV;                             // threads
-  static constexpr int NSTAGE = TBM == 256 ? 3 : 2;
-  static constexpr int STAGE = (TBM + BN) * BK * 2;               // bytes per LDS stage (A then B)
-  static constexpr int LDS = NSTAGE * STAGE > TBM * CROW * 2 ? NSTAGE * STAGE : TBM * CROW * 2;
+  static constexpr int STAGE = (TBM + TBN) * BK * 2;              // bytes per LDS stage (A then B)
+  static constexpr int CROWV = TBN + 8;                           // epilogue tile row (elements)
+  static constexpr int EROWS = TBM * CROWV * 2 <= NSTAGE * STAGE ? TBM : WR;   // epilogue rows per pass
+  static constexpr int LDS = NSTAGE * STAGE > EROWS * CROWV * 2 ? NSTAGE * STAGE : EROWS * CROWV * 2;
   static constexpr int ADMA = TBM / 8 / NWV;                      // A DMA instructions per wave per step: 4
-  static constexpr int BBLK = BN / 8;                             // 8-row B blocks per step: 20
-  static constexpr int BDMA = (BBLK + NWV - 1) / NWV;             // B DMA slots per wave: 5 | 3
+  static constexpr int BBLK = TBN / 8;                            // 8-row B blocks per step
+  static constexpr int BDMA = (BBLK + NWV - 1) / NWV;             // B DMA slots per wave
 };
-constexpr int G_STAGE = GCfg<128>::STAGE;
-constexpr int G_LDS = GCfg<128>::LDS;
-constexpr int G_ADMA = GCfg<128>::ADMA;
-constexpr int G_BDMA = GCfg<128>::BDMA;
+template <int CF> struct GCfg;
+template <> struct GCfg<0> : GTile<128, 160, 4, 2> {};
+template <> struct GCfg<1> : GTile<256, 160, 4, 3> {};
+template <> struct GCfg<2> : GTile<256, 320, 8, 2> {};
+constexpr int G_STAGE = GCfg<0>::STAGE;
+constexpr int G_LDS = GCfg<0>::LDS;
 
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
@@ -124,21 +135,22 @@ __device__ __forceinline__ float erf_fast(float x) {
 // the fly (per row: the source pixel's offset and the output pixel's parities; a tap's source row /
 // column step is -1, 0 or +1 by parity, two selects + adds per row and step); 0 = 64-bit pointers
 // rebuilt per step (inputs beyond 2^31 bytes).
-template <int KS, int EPI, int AM, int TBM>
+template <int KS, int EPI, int AM, int CF>
 __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
-  using Cfg = GCfg<TBM>;
+  using Cfg = GCfg<CF>;
+  static_assert(EPI != 1 || Cfg::TBN == 160, "GEGLU interleave is per 160-column tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / Cfg::WCOL, wn = w - (w / Cfg::WCOL) * Cfg::WCOL;
   // B blocks of this wave: 8 * (w + Cfg::NWV * i) for i < nbd (8 waves: waves 0-3 take three, 4-7 two)
   const int nbd = (Cfg::BBLK - w + Cfg::NWV - 1) / Cfg::NWV;
   const int M = a.batch * a.out_h * a.out_w;
-  const int ntn = a.cout / BN;
+  const int ntn = a.cout / Cfg::TBN;
   const int ks_n = EPI == 2 ? a.ksplit : 1;
   const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid0 % ks_n, bid = bid0 / ks_n;
   const int mt = bid / ntn, nt = bid - mt * ntn;
-  const int m0 = mt * TBM, n0 = nt * BN;
+  const int m0 = mt * Cfg::TBM, n0 = nt * Cfg::TBN;
   const bf16* x = static_cast<const bf16*>(a.x);
   const bf16* wt = static_cast<const bf16*>(a.w);
   const int Kw = KS * KS * a.cin;
@@ -195,7 +207,7 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     }
 #pragma unroll
     for (int i = 0; i < Cfg::BDMA; ++i) {
-      const int row = 8 * (w + Cfg::NWV * i) + lr < BN ? 8 * (w + Cfg::NWV * i) + lr : BN - 1;
+      const int row = 8 * (w + Cfg::NWV * i) + lr < Cfg::TBN ? 8 * (w + Cfg::NWV * i) + lr : Cfg::TBN - 1;
       b_off[i] = (uint32_t)(((n0 + row) * Kw + b_c[i]) * 2);
     }
   }
@@ -219,7 +231,7 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     const int tap = step / csteps, c0 = (step - tap * csteps) * BK;
     const int kh = tap / KS, kw = tap - kh * KS;
     char* As = smem + stage * Cfg::STAGE;
-    char* Bs = As + TBM * BK * 2;
+    char* Bs = As + Cfg::TBM * BK * 2;
     if constexpr (AM != 0) {
       if constexpr (AM == 2) {
         // source row step of tap row kh for output-row parity py: kh 0 -> py - 1, 1 -> 0, 2 -> py
@@ -278,9 +290,9 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     }
   };
 
-  f32x4v acc[WTM][WTN];
+  f32x4v acc[Cfg::WTM][WTN];
 #pragma unroll
-  for (int i = 0; i < WTM; ++i)
+  for (int i = 0; i < Cfg::WTM; ++i)
 #pragma unroll
     for (int j = 0; j < WTN; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
@@ -310,14 +322,14 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       if (step + 2 < s_end) dma(step + 2, cur == 0 ? 2 : cur - 1);
     }
     const char* As = smem + cur * Cfg::STAGE;
-    const char* Bs = As + TBM * BK * 2;
+    const char* Bs = As + Cfg::TBM * BK * 2;
     cur = cur + 1 == Cfg::NSTAGE ? 0 : cur + 1;
 #pragma unroll
     for (int ks = 0; ks < BK / 8; ks += 4) {      // chunk index of the k-step (0 or 4)
-      bf16x8 af[WTM], bfr[WTN];
+      bf16x8 af[Cfg::WTM], bfr[WTN];
 #pragma unroll
-      for (int i = 0; i < WTM; ++i) {
-        const int r = wm * 64 + 16 * i + fr;
+      for (int i = 0; i < Cfg::WTM; ++i) {
+        const int r = wm * Cfg::WR + 16 * i + fr;
         af[i] = *reinterpret_cast<const bf16x8*>(As + r * BK * 2 + swz(r, ks + fq) * 16);
       }
 #pragma unroll
@@ -326,7 +338,7 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
         bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK * 2 + swz(r, ks + fq) * 16);
       }
 #pragma unroll
-      for (int i = 0; i < WTM; ++i)
+      for (int i = 0; i < Cfg::WTM; ++i)
 #pragma unroll
         for (int j = 0; j < WTN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
@@ -336,10 +348,10 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     // fp32 slice: lane holds rows 4*fq+e of column fr of each 16x16 tile
     float* ws = a.workspace + (int64_t)split * M * a.cout;
 #pragma unroll
-    for (int i = 0; i < WTM; ++i)
+    for (int i = 0; i < Cfg::WTM; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int p = m0 + wm * 64 + 16 * i + 4 * fq + e;
+        const int p = m0 + wm * Cfg::WR + 16 * i + 4 * fq + e;
         if (p < M) {
 #pragma unroll
           for (int j = 0; j < WTN; ++j) ws[(int64_t)p * a.cout + n0 + wn * 80 + 16 * j + fr] = acc[i][j][e];
@@ -347,32 +359,38 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       }
     return;
   }
-  __syncthreads();
   bf16* Cs = reinterpret_cast<bf16*>(smem);
   const bf16* bias = static_cast<const bf16*>(a.bias);
-#pragma unroll
-  for (int j = 0; j < WTN; ++j) {
-    const int col = wn * 80 + 16 * j + fr;
-    const float bv = bias ? (float)bias[n0 + col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < WTM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        Cs[(wm * 64 + 16 * i + 4 * fq + e) * CROW + col] = (bf16)(acc[i][j][e] + bv);
-  }
-  __syncthreads();
   const bf16* res = static_cast<const bf16*>(a.residual);
   bf16* y = static_cast<bf16*>(a.y);
+  // rows [pass * EROWS, (pass + 1) * EROWS) of the tile go through the LDS tile at a time
+  for (int pass = 0; pass < Cfg::TBM / Cfg::EROWS; ++pass) {
+  __syncthreads();
+  if (wm * Cfg::WR / Cfg::EROWS == pass) {
+    const int rb = wm * Cfg::WR - pass * Cfg::EROWS;
+#pragma unroll
+    for (int j = 0; j < WTN; ++j) {
+      const int col = wn * 80 + 16 * j + fr;
+      const float bv = bias ? (float)bias[n0 + col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < Cfg::WTM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          Cs[(rb + 16 * i + 4 * fq + e) * Cfg::CROWV + col] = (bf16)(acc[i][j][e] + bv);
+    }
+  }
+  __syncthreads();
+  const int mp = m0 + pass * Cfg::EROWS;
   if constexpr (EPI == 1) {
 #pragma clang fp contract(off)
     constexpr float kAlpha = 0.70710678118654752440f;
     const int half = a.cout / 2;
-    for (int c = tid; c < TBM * (BN / 16); c += Cfg::NT) {
-      const int row = c / (BN / 16), ch = c - row * (BN / 16);
-      const int p = m0 + row;
+    for (int c = tid; c < Cfg::EROWS * (Cfg::TBN / 16); c += Cfg::NT) {
+      const int row = c / (Cfg::TBN / 16), ch = c - row * (Cfg::TBN / 16);
+      const int p = mp + row;
       if (p >= M) continue;
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
-      const bf16x8 gv = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + BN / 2 + ch * 8);
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + ch * 8);
+      const bf16x8 gv = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + Cfg::TBN / 2 + ch * 8);
       bf16x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -380,15 +398,15 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
         const float ge = (float)(bf16)(g * 0.5f * (1.f + erf_fast(g * kAlpha)));
         v[j] = (bf16)((float)av[j] * ge);
       }
-      *reinterpret_cast<bf16x8*>(y + (int64_t)p * half + nt * (BN / 2) + ch * 8) = v;
+      *reinterpret_cast<bf16x8*>(y + (int64_t)p * half + nt * (Cfg::TBN / 2) + ch * 8) = v;
     }
-    return;
+    continue;
   }
-  for (int c = tid; c < TBM * (BN / 8); c += Cfg::NT) {
-    const int row = c / (BN / 8), ch = c - row * (BN / 8);
-    const int p = m0 + row;
+  for (int c = tid; c < Cfg::EROWS * (Cfg::TBN / 8); c += Cfg::NT) {
+    const int row = c / (Cfg::TBN / 8), ch = c - row * (Cfg::TBN / 8);
+    const int p = mp + row;
     if (p >= M) continue;
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + ch * 8);
     const int64_t o = (int64_t)p * a.cout + n0 + ch * 8;
     if (res) {
       const bf16x8 rv = *reinterpret_cast<const bf16x8*>(res + o);
@@ -397,24 +415,33 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     }
     *reinterpret_cast<bf16x8*>(y + o) = v;
   }
+  }
 }
 
 template <int KS, int EPI = 0, int AM = 1>
 __global__ __launch_bounds__(256, 2) void conv_kernel_g(const vp2p_conv_args a) {
-  conv_tile<KS, EPI, AM, 128>(a);
+  conv_tile<KS, EPI, AM, 0>(a);
 }
 
 template <int KS, int EPI = 0, int AM = 1>
 __global__ __launch_bounds__(512, 1) void conv_kernel_b(const vp2p_conv_args a) {
-  conv_tile<KS, EPI, AM, 256>(a);
+  conv_tile<KS, EPI, AM, 1>(a);
 }
 
-template <int KS, int EPI, int AM, int TBM> struct ConvKernel;
-template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 128> {
+template <int KS, int EPI = 0, int AM = 1>
+__global__ __launch_bounds__(512, 1) void conv_kernel_w(const vp2p_conv_args a) {
+  conv_tile<KS, EPI, AM, 2>(a);
+}
+
+template <int KS, int EPI, int AM, int CF> struct ConvKernel;
+template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 0> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, AM>); }
 };
-template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 256> {
+template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 1> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_b<KS, EPI, AM>); }
+};
+template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 2> {
+  static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_w<KS, EPI, AM>); }
 };
 
 // split-K second pass: y = round(round(sum_s ws[s] + bias) + residual), the one-pass roundings
@@ -447,48 +474,57 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const vp2p_conv_args a
   *reinterpret_cast<bf16x8*>(static_cast<bf16*>(a.y) + o) = out;
 }
 
-template <int KS, int EPI, int AM, int TBM>
+template <int KS, int EPI, int AM, int CF>
 static int launch_g1(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
-  using Cfg = GCfg<TBM>;
-  static const bool attr = hipFuncSetAttribute(ConvKernel<KS, EPI, AM, TBM>::fn(),
+  using Cfg = GCfg<CF>;
+  static const bool attr = hipFuncSetAttribute(ConvKernel<KS, EPI, AM, CF>::fn(),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  if constexpr (TBM == 128)
+  if constexpr (CF == 0)
     hipLaunchKernelGGL((conv_kernel_g<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
-  else
+  else if constexpr (CF == 1)
     hipLaunchKernelGGL((conv_kernel_b<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
+  else
+    hipLaunchKernelGGL((conv_kernel_w<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
 // am: addressing form (see conv_kernel_g); the upsampling form exists for the 3x3 one-pass kernel only
-template <int KS, int EPI, int TBM = 128>
+template <int KS, int EPI, int CF = 0>
 static int launch_g(const vp2p_conv_args& a, dim3 grid, int am, hipStream_t s) {
   if constexpr (KS == 3 && EPI == 0)
-    if (am == 2) return launch_g1<KS, EPI, 2, TBM>(a, grid, s);
-  return am == 1 ? launch_g1<KS, EPI, 1, TBM>(a, grid, s) : launch_g1<KS, EPI, 0, TBM>(a, grid, s);
+    if (am == 2) return launch_g1<KS, EPI, 2, CF>(a, grid, s);
+  return am == 1 ? launch_g1<KS, EPI, 1, CF>(a, grid, s) : launch_g1<KS, EPI, 0, CF>(a, grid, s);
 }
 
-// The 256-row tile for one-pass launches that still fill the chip with one workgroup per CU.
-// Measured (profiles/r03_k10_tile_ab.jsonl, bit-equal outputs): it wins only on the long-K 1x1
-// GEMMs (M 131072, K 1280, N 320: 185.5 -> 170.2 us) and loses 2-8 % on the 3x3 convs and the
-// K = 320 GEMM / GEGLU shapes, whose per-tile prologue and epilogue no longer overlap a second
-// workgroup on the CU.  auto = 1x1 with K >= 1280 only.
-// VP2P_CONV_TILE=128 | 256 | auto (default) -- an A/B switch, read once.
-static int big_tile_mode() {
+// Tile choice for one-pass launches (split-K launches always take CF 0).
+// CF 1 (256 x 160, 3 stages): measured (profiles/r03_k10_tile_ab.jsonl, bit-equal) to win only on the
+// long-K 1x1 GEMMs (M 131072, K 1280, N 320: 185.5 -> 170.2 us), 2-8 % slower on the 3x3 convs and
+// the K = 320 GEMM / GEGLU shapes.  CF 2 (256 x 320 wide): Cout % 320 == 0, no GEGLU, and enough
+// tiles to give every CU one.  VP2P_CONV_TILE=128 | 256 | wide | auto (default) -- A/B, read once.
+static int tile_mode() {
   static const int m = [] {
     const char* e = getenv("VP2P_CONV_TILE");
     if (e && e[0] == '1') return 0;
     if (e && e[0] == '2') return 2;
+    if (e && e[0] == 'w') return 3;
     return 1;
   }();
   return m;
 }
 
-static bool use_big_tile(const vp2p_conv_args* a, int64_t M) {
-  const int mode = big_tile_mode();
-  if (mode == 0) return false;
-  const int64_t tiles = (M + 255) / 256 * (a->cout / BN);
-  return mode == 2 ? tiles >= 1 : (tiles >= 256 && a->kernel == 1 && a->cin >= 1280);
+static bool wide_auto(const vp2p_conv_args* a) { return a->kernel == 3; }
+
+static int pick_tile(const vp2p_conv_args* a, int64_t M) {
+  const int mode = tile_mode();
+  if (mode == 0) return 0;
+  const int64_t tiles_b = (M + 255) / 256 * (a->cout / BN);
+  const bool wide_ok = a->cout % 320 == 0 && a->epilogue == VP2P_CONV_EPI_NONE;
+  const int64_t tiles_w = (M + 255) / 256 * (a->cout / 320);
+  if (mode == 2) return 1;
+  if (mode == 3) return wide_ok ? 2 : 0;
+  if (wide_ok && tiles_w >= 256 && wide_auto(a)) return 2;
+  return (tiles_b >= 256 && a->kernel == 1 && a->cin >= 1280) ? 1 : 0;
 }
 
 // K-split for this shape: 1 unless the grid would leave most CUs idle (the 8x8-latent convs)
@@ -565,10 +601,13 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
     if (rc != VP2P_OK) return rc;
     const int64_t n = M * (a->cout / 8);
     hipLaunchKernelGGL(conv::conv_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
-  } else if (conv::use_big_tile(a, M)) {
+  } else if (const int cf = conv::pick_tile(a, M); cf == 1) {
     const dim3 gb((unsigned)((M + 255) / 256 * (a->cout / conv::BN)));
-    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 256>(*a, gb, fast, s);
-    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 256>(*a, gb, fast, s) : conv::launch_g<1, 0, 256>(*a, gb, fast, s);
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 1>(*a, gb, fast, s);
+    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 1>(*a, gb, fast, s) : conv::launch_g<1, 0, 1>(*a, gb, fast, s);
+  } else if (cf == 2) {
+    const dim3 gw((unsigned)((M + 255) / 256 * (a->cout / 320)));
+    rc = a->kernel == 3 ? conv::launch_g<3, 0, 2>(*a, gw, fast, s) : conv::launch_g<1, 0, 2>(*a, gw, fast, s);
   } else if (a->epilogue == VP2P_CONV_EPI_GEGLU) {
     rc = conv::launch_g<1, 1>(*a, grid, fast, s);
   } else {
