@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 11
+#define VP2P_ABI_VERSION 12
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -349,6 +349,11 @@ typedef struct vp2p_conv_args {
    * cin2); both % 64 == 0.  NULL / 0: x holds all cin channels. */
   const void* x2;
   int32_t cin2;
+  /* output scale of the one-pass / split-K epilogue without a residual: y = alpha * (x * w + bias),
+   * one rounding (the FrameAttention to_q projection pre-scaled by scale * log2 e for K1's folded
+   * max, torch.addmm(bias, x, w^T, beta=alpha, alpha=alpha) of the reference-precision path);
+   * 0 = 1 (zero-initialised callers). */
+  float alpha;
 } vp2p_conv_args;
 
 int vp2p_conv2d_supported(const vp2p_conv_args* args);

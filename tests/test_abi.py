@@ -75,3 +75,36 @@ def test_struct_layout_matches_header(tmp_path):
         py = structs[cname]
         want = ctypes.sizeof(py) if field == "size" else getattr(py, field).offset
         assert int(val) == want, (cname, field, val, want)
+
+
+def test_linear_alpha_rejects_residual_epilogue():
+    """The output scale is defined only for the plain epilogue: with a residual the shape is unsupported."""
+    import ctypes
+    from vp2p import _lib
+    lib = _lib.load()
+    a = _lib.ConvArgs(None, None, None, None, None, 1, 4096, 1, 320, 320, 4096, 1, 1, 1, 0, _lib.BF16,
+                      _lib.CONV_EPI_NONE)
+    assert lib.vp2p_conv2d_supported(ctypes.byref(a)) == 1
+    a.alpha = 0.5
+    assert lib.vp2p_conv2d_supported(ctypes.byref(a)) == 1
+    a.residual = 16
+    assert lib.vp2p_conv2d_supported(ctypes.byref(a)) == 0
+    a.residual = None
+    a.alpha = float("nan")
+    assert lib.vp2p_conv2d_supported(ctypes.byref(a)) == 0
+
+
+def test_linear_rule_table():
+    """The K10-vs-hipBLASLt projection choice is a fixed table of M ranges (no timing at run time)."""
+    from vp2p import ops
+    r = ops.LinearRule()
+    assert r.use_k10(131072, 320, 320)            # the res-64 projections (measured K10 0.71x hipBLASLt)
+    assert not r.use_k10(131072, 123, 456)        # pairs not in the table stay on the library
+    for k, runs in r.rules.items():
+        K, N = (int(t) for t in k.split("|"))
+        assert K % 64 == 0 and N % 160 == 0
+        for lo, hi in runs:
+            assert (lo is None or lo > 0) and (hi is None or lo is None or hi >= lo)
+    r.rules = {"640|640": [[None, 4096], [65536, 65536], [131072, None]]}
+    assert r.use_k10(10, 640, 640) and r.use_k10(4096, 640, 640) and not r.use_k10(8192, 640, 640)
+    assert r.use_k10(65536, 640, 640) and not r.use_k10(100000, 640, 640) and r.use_k10(10 ** 7, 640, 640)

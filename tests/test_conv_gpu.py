@@ -163,6 +163,29 @@ def test_linear_residual():
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("M,K,N,alpha", [(1000, 320, 320, 1.0), (70000, 320, 960, 1.0), (4100, 1280, 320, 0.2281),
+                                         (131072, 320, 320, 0.2281), (777, 640, 640, -3.5), (8192, 1280, 1280, 1.0)])
+def test_linear_k10_alpha(M, K, N, alpha):
+    """K10 plain projection alpha * (x W^T + b) (every tile the shape picks: wide 256 x 320, 128 x 160,
+    split-K) vs the fp32 GEMM on the same bf16 inputs, one rounding."""
+    from vp2p import ops
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    ref = alpha * F.linear(x.float(), w.float(), b.float())
+    with torch.no_grad():
+        assert ops.linear_k10_ok(x, w, b)
+        out = ops.linear_k10(x, w, b, alpha)
+    torch.cuda.synchronize()
+    assert out.shape == (M, N)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
+    if alpha == 1.0:       # alpha = 1 (and 0 = unset) is bit-equal to the unscaled epilogue
+        a2 = ops.linear_k10(x, w, b)
+        assert torch.equal(out, a2)
+
+
 @pytest.mark.parametrize("mode", ["k10", "library"])
 def test_attn_temp_residual_on_output_projection(mode):
     """attn_temp(y, residual=x) (the block's last add riding on to_out, attention.py:268) equals

@@ -74,30 +74,44 @@ constexpr int GBM = 128, NW = 4;                               // the split-K / 
 //     so the barrier does not drain the ring) -- the long-K 1x1 GEMMs;
 //  2: 256 x 320 "wide", 8 waves (2 x 4 of 128 x 80: 8 x 5 MFMA tiles, every A fragment used 5x,
 //     every B fragment 8x), two stages (2 x 72 KB), one workgroup per CU: twice the MFMAs per LDS
-//     byte read and per barrier of 0 / 1 (Cout % 320 == 0; the epilogue runs in two 128-row passes).
-// All: the same per-output K order and MFMA sequence, so bit-equal results.
-template <int TBM_, int TBN_, int WTM_, int NST_> struct GTile {
+//     byte read and per barrier of 0 / 1 (Cout % 320 == 0; the epilogue runs in two 128-row passes);
+//  3: the wide tile on 32-channel K-steps in a FOUR-stage ring (4 x 36 KB): the DMA of three steps in
+//     flight under the MFMAs of one (counted vmcnt + raw s_barrier), where the two-stage wide tile
+//     issues a step's DMA only one step ahead.  64-byte LDS rows; LDS slot j of row r holds global
+//     chunk j ^ S[(r >> 2) & 3], S = {0, 2, 3, 1}: the 16 rows of each 16-lane ds_read_b128 group
+//     (rows 0-15 once, chunks c or c + 1) then hit 16 distinct 4-bank groups.
+// All: the same per-output K order and MFMA sequence (one 16x16x32 MFMA per 32 channels), so
+// bit-equal results.
+template <int TBM_, int TBN_, int WTM_, int NST_, int KB_ = 64> struct GTile {
   static constexpr int TBM = TBM_, TBN = TBN_, WTM = WTM_, NSTAGE = NST_;
+  static constexpr int KB = KB_;                                  // channels per K-step
+  static constexpr int RB = KB * 2;                               // LDS row bytes
+  static constexpr int CPW = KB / 8;                              // 16-byte chunks per row
+  static constexpr int RPI = 64 / CPW;                            // rows per LDS-DMA instruction
+  __device__ static __forceinline__ int swz(int r, int c) {
+    if constexpr (KB == 64) return c ^ ((r >> 1) & 7);
+    else return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);
+  }
   static constexpr int WR = 16 * WTM;                             // output rows per wave
   static constexpr int WCOL = TBN / 80;                           // waves along N (80 columns each)
   static constexpr int NWV = (TBM / WR) * WCOL;                   // waves
   static constexpr int NT = 64 * NWV;                             // threads
-  static constexpr int STAGE = (TBM + TBN) * BK * 2;              // bytes per LDS stage (A then B)
+  static constexpr int STAGE = (TBM + TBN) * RB;                  // bytes per LDS stage (A then B)
   static constexpr int CROWV = TBN + 8;                           // epilogue tile row (elements)
   static constexpr int EROWS = TBM * CROWV * 2 <= NSTAGE * STAGE ? TBM : WR;   // epilogue rows per pass
   static constexpr int LDS = NSTAGE * STAGE > EROWS * CROWV * 2 ? NSTAGE * STAGE : EROWS * CROWV * 2;
-  static constexpr int ADMA = TBM / 8 / NWV;                      // A DMA instructions per wave per step: 4
-  static constexpr int BBLK = TBN / 8;                            // 8-row B blocks per step
+  static constexpr int ADMA = TBM / RPI / NWV;                    // A DMA instructions per wave per step
+  static constexpr int BBLK = TBN / RPI;                          // RPI-row B blocks per step
   static constexpr int BDMA = (BBLK + NWV - 1) / NWV;             // B DMA slots per wave
 };
 template <int CF> struct GCfg;
 template <> struct GCfg<0> : GTile<128, 160, 4, 2> {};
 template <> struct GCfg<1> : GTile<256, 160, 4, 3> {};
 template <> struct GCfg<2> : GTile<256, 320, 8, 2> {};
+template <> struct GCfg<3> : GTile<256, 320, 8, 4, 32> {};
 constexpr int G_STAGE = GCfg<0>::STAGE;
 constexpr int G_LDS = GCfg<0>::LDS;
 
-__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
 // LDS-DMA destination (a non-template helper: the address-space cast of a TBM-dependent expression
 // inside the kernel template makes hipcc's host pass silently drop the kernel's launch stub)
@@ -138,7 +152,7 @@ __device__ __forceinline__ float erf_fast(float x) {
 template <int KS, int EPI, int AM, int CF>
 __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   using Cfg = GCfg<CF>;
-  static_assert(EPI != 1 || Cfg::TBN == 160, "GEGLU interleave is per 160-column tile");
+  static_assert(EPI != 1 || Cfg::TBN % 160 == 0, "GEGLU interleave is per 160-column block");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w / Cfg::WCOL, wn = w - (w / Cfg::WCOL) * Cfg::WCOL;
@@ -156,13 +170,13 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   const int Kw = KS * KS * a.cin;
   const bf16* zero = reinterpret_cast<const bf16*>(kZero16);
 
-  // this lane's rows: A instruction i of wave w covers rows 8*(w + 4i) .. +7, lane row l / 8
-  const int lr = l >> 3, lj = l & 7;
+  // this lane's rows: A instruction i of wave w covers rows RPI*(w + NWV*i) .. +RPI-1, lane row l / CPW
+  const int lr = l / Cfg::CPW, lj = l % Cfg::CPW;
   int a_n[Cfg::ADMA], a_iy[Cfg::ADMA], a_ix[Cfg::ADMA], a_c[Cfg::ADMA];
   bool a_ok[Cfg::ADMA];
 #pragma unroll
   for (int i = 0; i < Cfg::ADMA; ++i) {
-    const int r = 8 * (w + Cfg::NWV * i) + lr;
+    const int r = Cfg::RPI * (w + Cfg::NWV * i) + lr;
     const int p = m0 + r;
     a_ok[i] = p < M;
     const int pp = a_ok[i] ? p : 0;
@@ -171,11 +185,11 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     a_n[i] = n;
     a_iy[i] = oy * a.stride - a.pad;
     a_ix[i] = ox * a.stride - a.pad;
-    a_c[i] = swz(r, lj) * 8;                                  // source channel offset of this lane
+    a_c[i] = Cfg::swz(r, lj) * 8;                             // source channel offset of this lane
   }
   int b_c[Cfg::BDMA];
 #pragma unroll
-  for (int i = 0; i < Cfg::BDMA; ++i) b_c[i] = swz(8 * (w + Cfg::NWV * i) + lr, lj) * 8;   // swz: (r >> 1) & 7 only
+  for (int i = 0; i < Cfg::BDMA; ++i) b_c[i] = Cfg::swz(Cfg::RPI * (w + Cfg::NWV * i) + lr, lj) * 8;
   // buffer forms: byte offsets at tap (0, 0) (AM 2: of the source pixel under the output pixel) and
   // the out-of-image tap masks (bit kh * KS + kw; AM 2: the output pixel's parities in bits 16, 17)
   uint32_t a_off[Cfg::ADMA], a_bad[Cfg::ADMA], b_off[Cfg::BDMA];
@@ -207,7 +221,7 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     }
 #pragma unroll
     for (int i = 0; i < Cfg::BDMA; ++i) {
-      const int row = 8 * (w + Cfg::NWV * i) + lr < Cfg::TBN ? 8 * (w + Cfg::NWV * i) + lr : Cfg::TBN - 1;
+      const int row = Cfg::RPI * (w + Cfg::NWV * i) + lr < Cfg::TBN ? Cfg::RPI * (w + Cfg::NWV * i) + lr : Cfg::TBN - 1;
       b_off[i] = (uint32_t)(((n0 + row) * Kw + b_c[i]) * 2);
     }
   }
@@ -224,14 +238,14 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
         a_off2[i] = (uint32_t)((((a_n[i] * a.in_h + a_iy[i]) * a.in_w + a_ix[i]) * a.cin2 + a_c[i]) * 2);
     }
   }
-  const int csteps = a.cin / BK;
+  const int csteps = a.cin / Cfg::KB;
   const int nall = KS * KS * csteps;
   const int s_begin = (int)((int64_t)nall * split / ks_n), s_end = (int)((int64_t)nall * (split + 1) / ks_n);
   auto dma = [&](int step, int stage) {
-    const int tap = step / csteps, c0 = (step - tap * csteps) * BK;
+    const int tap = step / csteps, c0 = (step - tap * csteps) * Cfg::KB;
     const int kh = tap / KS, kw = tap - kh * KS;
     char* As = smem + stage * Cfg::STAGE;
-    char* Bs = As + Cfg::TBM * BK * 2;
+    char* Bs = As + Cfg::TBM * Cfg::RB;
     if constexpr (AM != 0) {
       if constexpr (AM == 2) {
         // source row step of tap row kh for output-row parity py: kh 0 -> py - 1, 1 -> 0, 2 -> py
@@ -242,27 +256,27 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
 #pragma unroll
         for (int i = 0; i < Cfg::ADMA; ++i) {
           const uint32_t o = a_off[i] + xs + ((a_bad[i] >> 16) & 1 ? ry1 : ry0) + ((a_bad[i] >> 17) & 1 ? cx1 : cx0);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(As + 8 * (w + Cfg::NWV * i) * BK * 2),
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(As + Cfg::RPI * (w + Cfg::NWV * i) * Cfg::RB),
                                                    16, o | ((a_bad[i] >> tap) << 31), 0, 0, 0);
         }
       } else if (KS == 1 && a.x2 && c0 >= cin1) {           // 1x1, second source (wave-uniform)
         const uint32_t xs = (uint32_t)((c0 - cin1) * 2);
 #pragma unroll
         for (int i = 0; i < Cfg::ADMA; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr2, to_lds(As + 8 * (w + Cfg::NWV * i) * BK * 2),
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr2, to_lds(As + Cfg::RPI * (w + Cfg::NWV * i) * Cfg::RB),
                                                    16, (a_off2[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
       } else {
         const uint32_t xs = (uint32_t)(((kh * a.in_w + kw) * cin1 + c0) * 2);
 #pragma unroll
         for (int i = 0; i < Cfg::ADMA; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(As + 8 * (w + Cfg::NWV * i) * BK * 2),
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(As + Cfg::RPI * (w + Cfg::NWV * i) * Cfg::RB),
                                                    16, (a_off[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
       }
       const uint32_t ws = (uint32_t)((tap * a.cin + c0) * 2);
 #pragma unroll
       for (int i = 0; i < Cfg::BDMA; ++i)
         if (Cfg::BDMA * Cfg::NWV == Cfg::BBLK || i < nbd)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, to_lds(Bs + 8 * (w + Cfg::NWV * i) * BK * 2),
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, to_lds(Bs + Cfg::RPI * (w + Cfg::NWV * i) * Cfg::RB),
                                                    16, b_off[i] + ws, 0, 0, 0);
       return;
     }
@@ -276,16 +290,16 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       const bf16* src = ok ? x + (((int64_t)a_n[i] * (a.in_h >> up) + (iy >> up)) * (a.in_w >> up) + (ix >> up)) *
                                      a.cin + c0 + a_c[i]
                            : zero;
-      __builtin_amdgcn_global_load_lds(src, to_lds(As + 8 * (w + Cfg::NWV * i) * BK * 2),
+      __builtin_amdgcn_global_load_lds(src, to_lds(As + Cfg::RPI * (w + Cfg::NWV * i) * Cfg::RB),
                                        16, 0, 0);
     }
     const int64_t kofs = (int64_t)tap * a.cin + c0;
 #pragma unroll
     for (int i = 0; i < Cfg::BDMA; ++i) {
       if (Cfg::BDMA * Cfg::NWV != Cfg::BBLK && i >= nbd) continue;
-      const int row = 8 * (w + Cfg::NWV * i) + lr;
+      const int row = Cfg::RPI * (w + Cfg::NWV * i) + lr;
       const bf16* src = wt + (int64_t)(n0 + row) * Kw + kofs + b_c[i];
-      __builtin_amdgcn_global_load_lds(src, to_lds(Bs + 8 * (w + Cfg::NWV * i) * BK * 2),
+      __builtin_amdgcn_global_load_lds(src, to_lds(Bs + Cfg::RPI * (w + Cfg::NWV * i) * Cfg::RB),
                                        16, 0, 0);
     }
   };
@@ -297,45 +311,53 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     for (int j = 0; j < WTN; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
   const int fr = l & 15, fq = l >> 4;           // fragment row / 16-byte chunk within the 32-wide k-step
-  dma(s_begin, 0);
-  if constexpr (Cfg::NSTAGE == 3)
-    if (s_begin + 1 < s_end) dma(s_begin + 1, 1);
+  // prologue: the first NSTAGE - 1 steps' DMA in flight (one step for the two-stage tiles)
+#pragma unroll
+  for (int k = 0; k < Cfg::NSTAGE - 1; ++k)
+    if (s_begin + k < s_end) dma(s_begin + k, k);
+  // this wave's LDS-DMA instructions per step (the B blocks do not always split evenly over waves)
+  constexpr int CNT_HI = Cfg::ADMA + Cfg::BDMA, CNT_LO = Cfg::BBLK % Cfg::NWV == 0 ? CNT_HI : CNT_HI - 1;
+  const bool hi = w < Cfg::BBLK % Cfg::NWV || Cfg::BBLK % Cfg::NWV == 0;
   int cur = 0;                                    // LDS stage of this step
   for (int step = s_begin; step < s_end; ++step) {
     if constexpr (Cfg::NSTAGE == 2) {
       __syncthreads();                            // vmcnt(0): step's DMA landed; step-1's reads done
       if (step + 1 < s_end) dma(step + 1, cur ^ 1);
     } else {
-      // this wave's DMA of `step` landed (the one of step + 1 may stay in flight: in-order vmcnt),
-      // then every wave's: the barrier also orders all reads of stage (step - 1) % 3 before the
-      // DMA of step + 2 overwrites it.  A raw s_barrier: __syncthreads() would drain the ring.
-      if (step + 1 < s_end) {
-        if (w < Cfg::BBLK % Cfg::NWV || Cfg::BBLK % Cfg::NWV == 0)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::ADMA + Cfg::BDMA) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::ADMA + Cfg::BDMA - 1) : "memory");
+      // this wave's DMA of `step` landed (the ones of the next steps may stay in flight: in-order
+      // vmcnt), then every wave's: the barrier also orders all reads of stage (step - 1) % NSTAGE
+      // before the DMA of step + NSTAGE - 1 overwrites it.  A raw s_barrier: __syncthreads() would
+      // drain the ring.
+      const int ahead = min(Cfg::NSTAGE - 2, s_end - 1 - step);   // later steps already issued
+      if (ahead >= 2) {
+        if (hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CNT_HI) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CNT_LO) : "memory");
+      } else if (ahead == 1) {
+        if (hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT_HI) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT_LO) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (step + 2 < s_end) dma(step + 2, cur == 0 ? 2 : cur - 1);
+      if (step + Cfg::NSTAGE - 1 < s_end)
+        dma(step + Cfg::NSTAGE - 1, cur == 0 ? Cfg::NSTAGE - 1 : cur - 1);
     }
     const char* As = smem + cur * Cfg::STAGE;
-    const char* Bs = As + Cfg::TBM * BK * 2;
+    const char* Bs = As + Cfg::TBM * Cfg::RB;
     cur = cur + 1 == Cfg::NSTAGE ? 0 : cur + 1;
 #pragma unroll
-    for (int ks = 0; ks < BK / 8; ks += 4) {      // chunk index of the k-step (0 or 4)
+    for (int ks = 0; ks < Cfg::CPW; ks += 4) {   // chunk index of the 32-channel MFMA k-step (0 or 4)
       bf16x8 af[Cfg::WTM], bfr[WTN];
 #pragma unroll
       for (int i = 0; i < Cfg::WTM; ++i) {
         const int r = wm * Cfg::WR + 16 * i + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(As + r * BK * 2 + swz(r, ks + fq) * 16);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * Cfg::RB + Cfg::swz(r, ks + fq) * 16);
       }
 #pragma unroll
       for (int j = 0; j < WTN; ++j) {
         const int r = wn * 80 + 16 * j + fr;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK * 2 + swz(r, ks + fq) * 16);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * Cfg::RB + Cfg::swz(r, ks + fq) * 16);
       }
 #pragma unroll
       for (int i = 0; i < Cfg::WTM; ++i)
@@ -361,6 +383,7 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   }
   bf16* Cs = reinterpret_cast<bf16*>(smem);
   const bf16* bias = static_cast<const bf16*>(a.bias);
+  const float al = a.alpha == 0.f ? 1.f : a.alpha;     // x 1.0f is exact: alpha-free callers unchanged
   const bf16* res = static_cast<const bf16*>(a.residual);
   bf16* y = static_cast<bf16*>(a.y);
   // rows [pass * EROWS, (pass + 1) * EROWS) of the tile go through the LDS tile at a time
@@ -376,7 +399,7 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       for (int i = 0; i < Cfg::WTM; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          Cs[(rb + 16 * i + 4 * fq + e) * Cfg::CROWV + col] = (bf16)(acc[i][j][e] + bv);
+          Cs[(rb + 16 * i + 4 * fq + e) * Cfg::CROWV + col] = (bf16)((acc[i][j][e] + bv) * al);
     }
   }
   __syncthreads();
@@ -389,8 +412,11 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       const int row = c / (Cfg::TBN / 16), ch = c - row * (Cfg::TBN / 16);
       const int p = mp + row;
       if (p >= M) continue;
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + ch * 8);
-      const bf16x8 gv = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + Cfg::TBN / 2 + ch * 8);
+      // 160-column block blk of the tile = [80 value | 80 gate] columns; its outputs are the
+      // 80 columns (nt * TBN / 160 + blk) * 80 + [0, 80) of y, i.e. nt * TBN / 2 + ch * 8 + [0, 8)
+      const int blk = ch / 10, cc = ch - blk * 10;
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + blk * 160 + cc * 8);
+      const bf16x8 gv = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + blk * 160 + 80 + cc * 8);
       bf16x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -433,6 +459,11 @@ __global__ __launch_bounds__(512, 1) void conv_kernel_w(const vp2p_conv_args a) 
   conv_tile<KS, EPI, AM, 2>(a);
 }
 
+template <int KS, int EPI = 0, int AM = 1>
+__global__ __launch_bounds__(512, 1) void conv_kernel_d(const vp2p_conv_args a) {
+  conv_tile<KS, EPI, AM, 3>(a);
+}
+
 template <int KS, int EPI, int AM, int CF> struct ConvKernel;
 template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 0> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, AM>); }
@@ -442,6 +473,9 @@ template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 1> {
 };
 template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 2> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_w<KS, EPI, AM>); }
+};
+template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 3> {
+  static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_d<KS, EPI, AM>); }
 };
 
 // split-K second pass: y = round(round(sum_s ws[s] + bias) + residual), the one-pass roundings
@@ -464,10 +498,11 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const vp2p_conv_args a
   }
   const bf16* bias = static_cast<const bf16*>(a.bias);
   const bf16* res = static_cast<const bf16*>(a.residual);
+  const float al = a.alpha == 0.f ? 1.f : a.alpha;
   bf16x8 out;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    float t = (float)(bf16)(v[j] + (bias ? (float)bias[c0 + j] : 0.f));
+    float t = (float)(bf16)((v[j] + (bias ? (float)bias[c0 + j] : 0.f)) * al);
     if (res) t = t + (float)res[o + j];
     out[j] = (bf16)t;
   }
@@ -484,8 +519,10 @@ static int launch_g1(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL((conv_kernel_g<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   else if constexpr (CF == 1)
     hipLaunchKernelGGL((conv_kernel_b<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
-  else
+  else if constexpr (CF == 2)
     hipLaunchKernelGGL((conv_kernel_w<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
+  else
+    hipLaunchKernelGGL((conv_kernel_d<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
@@ -501,28 +538,33 @@ static int launch_g(const vp2p_conv_args& a, dim3 grid, int am, hipStream_t s) {
 // CF 1 (256 x 160, 3 stages): measured (profiles/r03_k10_tile_ab.jsonl, bit-equal) to win only on the
 // long-K 1x1 GEMMs (M 131072, K 1280, N 320: 185.5 -> 170.2 us), 2-8 % slower on the 3x3 convs and
 // the K = 320 GEMM / GEGLU shapes.  CF 2 (256 x 320 wide): Cout % 320 == 0, no GEGLU, and enough
-// tiles to give every CU one.  VP2P_CONV_TILE=128 | 256 | wide | auto (default) -- A/B, read once.
+// tiles to give every CU one.  VP2P_CONV_TILE=128 | 256 | wide | deep | auto (default) -- A/B, read once.
 static int tile_mode() {
   static const int m = [] {
     const char* e = getenv("VP2P_CONV_TILE");
     if (e && e[0] == '1') return 0;
     if (e && e[0] == '2') return 2;
     if (e && e[0] == 'w') return 3;
+    if (e && e[0] == 'd') return 4;
     return 1;
   }();
   return m;
 }
 
-static bool wide_auto(const vp2p_conv_args* a) { return a->kernel == 3; }
+// auto: the wide tile wherever it gives every CU a tile (measured, profiles/r03_k10_wide_ab.jsonl,
+// bit-equal: 3x3 convs at 64^2 / 32^2 -6..-13 %, 1x1 GEMMs M 131072 K 320 / 1280 N 320 -5 / -21 %,
+// M 32768 K 640 N 640 -10 %; slower where it leaves CUs idle: 128-tile grids +3..+50 %)
+static bool wide_auto(const vp2p_conv_args* a) { return a->kernel == 3 || a->kernel == 1; }
 
 static int pick_tile(const vp2p_conv_args* a, int64_t M) {
   const int mode = tile_mode();
   if (mode == 0) return 0;
   const int64_t tiles_b = (M + 255) / 256 * (a->cout / BN);
-  const bool wide_ok = a->cout % 320 == 0 && a->epilogue == VP2P_CONV_EPI_NONE;
+  const bool wide_ok = a->cout % 320 == 0;    // plain and GEGLU epilogues (GEGLU: profiles/r03_k10_geglu_wide_ab.jsonl)
   const int64_t tiles_w = (M + 255) / 256 * (a->cout / 320);
   if (mode == 2) return 1;
-  if (mode == 3) return wide_ok ? 2 : 0;
+  if (mode == 3) return a->cout % 320 == 0 ? 2 : 0;   // GEGLU included (A/B)
+  if (mode == 4) return a->cout % 320 == 0 ? 3 : 0;
   if (wide_ok && tiles_w >= 256 && wide_auto(a)) return 2;
   return (tiles_b >= 256 && a->kernel == 1 && a->cin >= 1280) ? 1 : 0;
 }
@@ -556,6 +598,9 @@ extern "C" int vp2p_conv2d_supported(const vp2p_conv_args* a) {
   if (a->out_w != (a->in_w + 2 * a->pad - a->kernel) / a->stride + 1) return 0;
   if (a->epilogue != VP2P_CONV_EPI_NONE &&
       (a->epilogue != VP2P_CONV_EPI_GEGLU || a->kernel != 1 || a->stride != 1 || a->residual)) return 0;
+  // an output scale only on the plain epilogue without a residual (the scaled projection)
+  if (a->alpha != 0.f && a->alpha != 1.f && (a->residual || a->epilogue != VP2P_CONV_EPI_NONE)) return 0;
+  if (!(a->alpha == a->alpha) || a->alpha > 3.0e38f || a->alpha < -3.0e38f) return 0;   // NaN / inf
   if (a->upsample != 0 && (a->upsample != 1 || a->stride != 1 || (a->in_h & 1) || (a->in_w & 1))) return 0;
   if (a->x2 || a->cin2) {   // two-source input: 1x1 convs on the buffer-offset form only
     if (!a->x2 || a->cin2 <= 0 || a->cin2 >= a->cin || a->cin2 % conv::BK || a->kernel != 1 || a->stride != 1 ||
@@ -607,7 +652,12 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
     else rc = a->kernel == 3 ? conv::launch_g<3, 0, 1>(*a, gb, fast, s) : conv::launch_g<1, 0, 1>(*a, gb, fast, s);
   } else if (cf == 2) {
     const dim3 gw((unsigned)((M + 255) / 256 * (a->cout / 320)));
-    rc = a->kernel == 3 ? conv::launch_g<3, 0, 2>(*a, gw, fast, s) : conv::launch_g<1, 0, 2>(*a, gw, fast, s);
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 2>(*a, gw, fast, s);
+    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 2>(*a, gw, fast, s) : conv::launch_g<1, 0, 2>(*a, gw, fast, s);
+  } else if (cf == 3) {
+    const dim3 gw((unsigned)((M + 255) / 256 * (a->cout / 320)));
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 3>(*a, gw, fast, s);
+    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 3>(*a, gw, fast, s) : conv::launch_g<1, 0, 3>(*a, gw, fast, s);
   } else if (a->epilogue == VP2P_CONV_EPI_GEGLU) {
     rc = conv::launch_g<1, 1>(*a, grid, fast, s);
   } else {

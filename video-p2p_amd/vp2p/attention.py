@@ -11,7 +11,8 @@ of ptp_utils.py:196-221 on the HIP kernels:
 * FrameAttention (attn1, never hooked in the reference: its class name differs,
   ptp_utils.py:237) -> K1 ``vp2p_frame_attn_fwd``
 
-Projections stay on hipBLASLt GEMMs (``F.linear``); K/V of attn1 are projected for frame 0 only,
+Projections go through ``ops.linear`` (K10's GEMM core where the in-tree table measured it faster,
+hipBLASLt elsewhere); K/V of attn1 are projected for frame 0 only,
 K/V of attn2 once per batch row instead of once per frame, and attn_temp's q/k/v come from one GEMM
 against the concatenated weights -- all bit-identical to the reference's per-row projections.
 """
@@ -36,16 +37,6 @@ def _cat_weight(module: nn.Module, names, cache_attr: str) -> torch.Tensor:
     cat = torch.cat([w.detach() for w in ws], 0).contiguous()
     object.__setattr__(module, cache_attr, (key, cat))
     return cat
-
-
-def _scaled_linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], alpha: float) -> torch.Tensor:
-    """alpha * (x @ w^T + b) as ONE library GEMM (alpha and beta in its epilogue, one rounding)."""
-    x2 = x.reshape(-1, x.shape[-1])
-    if b is None:
-        y = torch.addmm(x2.new_zeros(()), x2, w.t(), beta=0, alpha=alpha)
-    else:
-        y = torch.addmm(b, x2, w.t(), beta=alpha, alpha=alpha)
-    return y.view(*x.shape[:-1], w.shape[0])
 
 
 class CrossAttention(nn.Module):
@@ -110,8 +101,8 @@ class FrameAttention(CrossAttention):
         else:
             # the softmax scale (times log2 e) rides in the projection GEMM's alpha: one rounding of
             # q' = c * (x W^T + b), and K1 runs its folded-max form (frame_attn.hip)
-            q = _scaled_linear(x, self.to_q.weight, self.to_q.bias,
-                               ops.frame_query_scale(self.to_q.weight.shape[0] // self.heads, self.scale))
+            q = ops.linear(x, self.to_q.weight, self.to_q.bias,
+                           alpha=ops.frame_query_scale(self.to_q.weight.shape[0] // self.heads, self.scale))
             prescaled = True
         C = q.shape[-1]
         if not prescaled:
@@ -134,10 +125,10 @@ class FrameAttention(CrossAttention):
                 raise RuntimeError("frame-sharded FrameAttention reached the inference path without "
                                    "the frame-0 broadcast")
             x0 = x.view(B, f, *x.shape[1:])[:, 0]
-        kv = F.linear(x0, wkv, bkv)
+        kv = ops.linear(x0, wkv, bkv)
         out = ops.frame_attention(q, kv[..., :C], kv[..., C:], f, self.heads, scale=self.scale,
                                   q_prescaled=True)
-        return self.to_out[1](self.to_out[0](out))
+        return self.to_out[1](_linear_out(self.to_out[0], out))
 
 
 def _batch_frames(x, controller, video_length):
@@ -188,7 +179,7 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
             return to_out(autograd.SharedKVAttention.apply(q, kv, f, h, module.scale))
         q = ops.linear(x, module.to_q.weight, module.to_q.bias)
         # K and V of the (B, 77, Cctx) context in one GEMM against [Wk; Wv]; K2's prep reads the views
-        kv = F.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
+        kv = ops.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
                       None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))
         Ck = module.to_k.weight.shape[0]
         k, v = kv[..., :Ck], kv[..., Ck:]
@@ -210,7 +201,7 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
             out = _pv(module, attn, v.contiguous(), B, f)
         elif controller is not None:
             controller.fused_end(True, place, call, probs)
-        return to_out(out)
+        return _linear_out(to_out, out)
 
     # self attention on the hooked path = temporal attention (attn_temp)
     C = module.to_q.weight.shape[0]
@@ -218,7 +209,7 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
     bias = None
     if module.to_q.bias is not None:
         bias = torch.cat([module.to_q.bias, module.to_k.bias, module.to_v.bias])
-    qkv = F.linear(x, w, bias)
+    qkv = ops.linear(x, w, bias)
     if autograd.needs_grad(qkv):
         if not plain or temporal_layout != "bf":
             raise NotImplementedError("backward through a P2P-controlled or '(b d) f c' temporal attention")
@@ -266,6 +257,14 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
     if shard is not None:
         out = shard.to_frames(out, B)
     return _out_proj(to_out, out, residual)
+
+
+def _linear_out(to_out, out):
+    """``to_out(out)`` at inference through ``ops.linear`` (K10's GEMM core for the K = 320 projections
+    of the 64x64 latents, hipBLASLt elsewhere); any other module, or autograd, calls it as is."""
+    if isinstance(to_out, nn.Linear) and not torch.is_grad_enabled():
+        return ops.linear(out, to_out.weight, to_out.bias)
+    return to_out(out)
 
 
 def _out_proj(to_out, out, residual):

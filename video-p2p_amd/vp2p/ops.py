@@ -773,25 +773,86 @@ def linear_residual(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.
     return y
 
 
-LINEAR_K10_MAX_N = int(os.environ.get("VP2P_LINEAR_K10_MAX_N", "640"))    # A/B knob, read once
+class LinearRule:
+    """Which plain projections run on K10's GEMM core instead of hipBLASLt: per (K, N), the ranges of
+    row counts M over which K10 measured faster (``linear_rules`` in the in-tree
+    ``miopen_db/kernel_choices.json``, written by ``tools/linear_choose.py`` on the MI355X from
+    profiles/r03_linear_choose.jsonl).  A range [lo, hi] covers the measured M between lo and hi; a
+    range that starts at the smallest measured M extends down to 0 and one that ends at the largest
+    extends up without bound.  A fixed table, so the kernel (and the numerics: K10 and hipBLASLt are
+    not bit-equal at every shape) is the same on every run, box and rank; pairs missing from it stay on
+    hipBLASLt.  ``VP2P_LINEAR``: ``table`` (default) | ``k10`` | ``library`` -- A/B, read once."""
+
+    DEFAULT = {"320|320": [[65536, None]], "320|640": [[65536, None]]}   # round 2's rule, no table
+
+    def __init__(self):
+        self.mode = os.environ.get("VP2P_LINEAR", "table")
+        if self.mode not in ("table", "k10", "library"):
+            raise ValueError(f"VP2P_LINEAR={self.mode!r}: expected table | k10 | library")
+        self.rules = dict(self.DEFAULT)
+        if os.path.exists(ConvSelector.TABLE):
+            with open(ConvSelector.TABLE) as fh:
+                table = json.load(fh).get("linear_rules")
+            if table is not None:
+                self.rules = {k: [list(r) for r in v] for k, v in table.items()}
+
+    def use_k10(self, M: int, K: int, N: int) -> bool:
+        if self.mode != "table":
+            return self.mode == "k10"
+        for lo, hi in self.rules.get(f"{K}|{N}", ()):
+            if (lo is None or M >= lo) and (hi is None or M <= hi):
+                return True
+        return False
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """x @ W^T + b (nn.Linear).  The K = 320 projections of the 64x64 latents (M >= 64k rows, N <= 640:
-    attn2's to_q and Transformer3DModel.proj_in at res-64) run on K10's GEMM core, measured faster than
-    hipBLASLt there (profiles/r02_linear_plain_ab.jsonl); every other shape, and anything that needs
-    a gradient, stays on hipBLASLt (F.linear).  A fixed shape rule: the same kernel every run."""
+LINEAR = LinearRule()
+
+
+def linear_k10_ok(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> bool:
+    """K10's GEMM core takes x @ W^T (+ b): bf16, contiguous, K % 64 == 0, N % 160 == 0, no autograd."""
+    return (x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.is_cuda and x.dim() >= 2
+            and not torch.is_grad_enabled() and x.is_contiguous() and weight.is_contiguous()
+            and (bias is None or (bias.dtype == x.dtype and bias.is_contiguous()))
+            and x.shape[-1] % 64 == 0 and weight.shape[0] % 160 == 0 and x.numel() > 0)
+
+
+def linear_k10(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+               alpha: float = 1.0) -> torch.Tensor:
+    """alpha * (x @ W^T + b) on K10's GEMM core (a 1x1 convolution over M = rows pixels), one rounding."""
+    K, N = x.shape[-1], weight.shape[0]
+    M = x.numel() // K
+    y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
+    a = _lib.ConvArgs(_ptr(x), _ptr(weight), _ptr(bias), None, _ptr(y), 1, M, 1, K, N, M, 1, 1, 1, 0,
+                      _lib.BF16, _lib.CONV_EPI_NONE)
+    a.alpha = float(alpha)
+    lib = _lib.load()
+    ws = None
+    wsb = lib.vp2p_conv2d_workspace_bytes(ctypes.byref(a))
+    if wsb > 0:
+        ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
+        a.workspace = _ptr(ws)
+    check(lib.vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd(linear)")
+    return y
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           alpha: Optional[float] = None) -> torch.Tensor:
+    """nn.Linear (``alpha``: alpha * (x @ W^T + b), one rounding -- the pre-scaled FrameAttention query).
+    K10's GEMM core where ``LINEAR`` says it is faster for the shape, hipBLASLt elsewhere and for
+    anything that needs a gradient."""
     K, N = x.shape[-1], weight.shape[0]
     M = x.numel() // max(K, 1)
-    if (K == 320 and N <= LINEAR_K10_MAX_N and M >= 65536 and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
-            and x.is_cuda and not torch.is_grad_enabled() and x.is_contiguous() and weight.is_contiguous()
-            and (bias is None or bias.dtype == x.dtype) and N % 160 == 0):
-        y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
-        a = _lib.ConvArgs(_ptr(x), _ptr(weight), _ptr(bias), None, _ptr(y), 1, M, 1, K, N, M, 1, 1, 1, 0,
-                          _lib.BF16, _lib.CONV_EPI_NONE)
-        check(_lib.load().vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd(linear)")
-        return y
-    return F.linear(x, weight, bias)
+    if linear_k10_ok(x, weight, bias) and LINEAR.use_k10(M, K, N):
+        return linear_k10(x, weight, bias, 1.0 if alpha is None else alpha)
+    if alpha is None:
+        return F.linear(x, weight, bias)
+    # one library GEMM with alpha and beta in its epilogue
+    x2 = x.reshape(-1, K)
+    if bias is None:
+        y = torch.addmm(x2.new_zeros(()), x2, weight.t(), beta=0, alpha=alpha)
+    else:
+        y = torch.addmm(bias, x2, weight.t(), beta=alpha, alpha=alpha)
+    return y.view(*x.shape[:-1], N)
 
 
 def linear_residual_supported(x: torch.Tensor, weight: torch.Tensor, residual: torch.Tensor) -> bool:
