@@ -125,6 +125,26 @@ __device__ __forceinline__ __attribute__((address_space(3))) void* to_lds(const 
 // mixed waves (~45 VALU per element): res-64 GEGLU projection 0.483 -> 0.432 ms, res-32 0.315 ->
 // 0.284 (profiles/r02_k10_epilogue_ab.jsonl; a transposed-accumulator epilogue with 8-byte LDS
 // writes measured no faster and was dropped).
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+// erf_fast on a pair: the same fp32 operations per element, on packed FMAs / multiplies (v_pk_fma_f32,
+// v_pk_mul_f32: two lanes' worth per instruction), so the GEGLU epilogue's polynomial costs half
+__device__ __forceinline__ f32x2v erf_fast2(f32x2v x) {
+  const f32x2v ax = __builtin_elementwise_abs(x);
+  f32x2v p = __builtin_elementwise_fma(ax, (f32x2v)(4.30638e-5f), (f32x2v)(2.765672e-4f));
+  p = __builtin_elementwise_fma(p, ax, (f32x2v)(1.520143e-4f));
+  p = __builtin_elementwise_fma(p, ax, (f32x2v)(9.2705272e-3f));
+  p = __builtin_elementwise_fma(p, ax, (f32x2v)(4.22820123e-2f));
+  p = __builtin_elementwise_fma(p, ax, (f32x2v)(7.05230784e-2f));
+  p = __builtin_elementwise_fma(p, ax, (f32x2v)(1.f));
+  p *= p;
+  p *= p;
+  p *= p;
+  p *= p;
+  const f32x2v r = {__builtin_amdgcn_rcpf(p.x), __builtin_amdgcn_rcpf(p.y)};
+  return __builtin_elementwise_copysign((f32x2v)(1.f) - r, x);
+}
+
 __device__ __forceinline__ float erf_fast(float x) {
   const float ax = fabsf(x);
   float p = __builtin_fmaf(ax, 4.30638e-5f, 2.765672e-4f);
@@ -419,10 +439,13 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       const bf16x8 gv = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + blk * 160 + 80 + cc * 8);
       bf16x8 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float g = (float)gv[j];
-        const float ge = (float)(bf16)(g * 0.5f * (1.f + erf_fast(g * kAlpha)));
-        v[j] = (bf16)((float)av[j] * ge);
+      for (int j = 0; j < 8; j += 2) {    // erf_fast's operations in pairs: bit-equal to the scalar form
+        const f32x2v g = {(float)gv[j], (float)gv[j + 1]};
+        const f32x2v gl = g * 0.5f * (1.f + erf_fast2(g * kAlpha));
+        const f32x2v ge = {(float)(bf16)gl.x, (float)(bf16)gl.y};
+        const f32x2v o = f32x2v{(float)av[j], (float)av[j + 1]} * ge;
+        v[j] = (bf16)o.x;
+        v[j + 1] = (bf16)o.y;
       }
       *reinterpret_cast<bf16x8*>(y + (int64_t)p * half + nt * (Cfg::TBN / 2) + ch * 8) = v;
     }

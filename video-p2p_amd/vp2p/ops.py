@@ -211,10 +211,12 @@ def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frame
                         plan: Optional[CrossEditPlan] = None, step: int = 0, edit: bool = True,
                         lb_acc: Optional[torch.Tensor] = None, probs_out: Optional[torch.Tensor] = None,
                         scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
-                        prompts: int = 0, cond_only: bool = False) -> torch.Tensor:
+                        prompts: int = 0, cond_only: bool = False,
+                        kv_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Hooked attn2 (ptp_utils.py:196-221) with the controller edit fused.  q: (B*f, N, C);
     k, v: the projected context (B, Nk, C) shared by all frames of a batch row.  ``cond_only``: the
-    batch is only the conditional half (B = prompts; a CFG-split rank)."""
+    batch is only the conditional half (B = prompts; a CFG-split rank).  ``kv_ws``: k / v already laid
+    out by ``cross_kv_prep`` (the caller caches it while the context is unchanged)."""
     dt = _dtype(q, k, v)
     Bf, N, C = q.shape
     B = Bf // frames
@@ -222,7 +224,7 @@ def cross_attention_p2p(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, frame
         raise ValueError("k/v must be (B, Nk, C)")
     d = C // heads
     nkv = k.shape[1]
-    ws = cross_kv_prep(k, v, heads)
+    ws = cross_kv_prep(k, v, heads) if kv_ws is None else kv_ws
     if out is None:
         out = torch.empty_like(q, memory_format=torch.contiguous_format)
     q_sb, q_sf, q_sn = _bf_strides(q, frames)

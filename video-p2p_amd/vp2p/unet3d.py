@@ -484,15 +484,31 @@ class UNet3DConditionModel(nn.Module):
             t = t[None].to(sample.device)
         t = t.expand(B)
         emb = self.time_embedding(self.time_proj(t).to(self.dtype))
-        ctx = encoder_hidden_states.to(self.dtype)
         if torch.is_grad_enabled():
-            return self._forward(sample, emb, ctx, return_dict)
+            return self._forward(sample, emb, encoder_hidden_states.to(self.dtype), return_dict)
+        ctx = self._context(encoder_hidden_states)
         self._project_temb(emb)
         try:
             return self._forward(sample, emb, ctx, return_dict)
         finally:
             for r in self.__dict__["_resnets"]:
                 object.__setattr__(r, "_temb_pre", None)
+
+    def _context(self, eh: torch.Tensor) -> torch.Tensor:
+        """``encoder_hidden_states`` in the UNet's dtype, ONE tensor object while the input is unchanged
+        (same storage, shape, strides and version): the attn2 layers then keep their context K / V and
+        K2 layout across the denoising steps (``attention._context_kv``)."""
+        if torch.cuda.is_current_stream_capturing():      # a HIP graph re-reads its input at every replay
+            return eh.to(self.dtype)
+        key = (eh.data_ptr(), tuple(eh.shape), tuple(eh.stride()), eh.dtype, eh.device, eh._version, self.dtype)
+        hit = self.__dict__.get("_ctx_cache")
+        if hit is not None and hit[0] == key:
+            return hit[2]
+        ctx = eh.to(self.dtype)
+        if ctx is eh:                       # already the UNet's dtype: a private copy, so that a later
+            ctx = eh.clone()                # in-place write to the caller's tensor cannot alias it
+        object.__setattr__(self, "_ctx_cache", (key, eh, ctx))
+        return ctx
 
     def _project_temb(self, emb):
         """Every resnet's ``time_emb_proj(silu(temb))`` (resnet.py:185-188) as ONE GEMM against the
