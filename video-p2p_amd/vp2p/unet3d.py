@@ -427,6 +427,9 @@ class UpBlock3D(_UpBlock):
         self.attentions = None
 
 
+_T_CACHE = os.environ.get("VP2P_T_CACHE", "1") != "0"     # A/B switch (0: a new H2D copy per forward)
+
+
 class UNet3DConditionModel(nn.Module):
     """unet.py:38-414 with SD-1.5 geometry by default (cross_attention_dim 768, 8 heads)."""
 
@@ -479,7 +482,13 @@ class UNet3DConditionModel(nn.Module):
         B, Cin, f, H, W = sample.shape
         t = timestep
         if not torch.is_tensor(t):
-            t = torch.tensor([t], dtype=torch.int64, device=sample.device)
+            # one device tensor per (timestep, device), made on first use: a per-forward
+            # torch.tensor(..., device=cuda) is a blocking H2D copy that drains the stream every step
+            tc = self.__dict__.setdefault("_t_dev", {})
+            key = (int(t), sample.device)
+            if key not in tc or not _T_CACHE:
+                tc[key] = torch.tensor([int(t)], dtype=torch.int64, device=sample.device)
+            t = tc[key]
         elif t.dim() == 0:
             t = t[None].to(sample.device)
         t = t.expand(B)
