@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 12
+#define VP2P_ABI_VERSION 13
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -328,8 +328,8 @@ int vp2p_geglu_bwd(const void* x, const void* dy, void* dx, int64_t rows, int32_
 enum vp2p_conv_epilogue {
   VP2P_CONV_EPI_NONE = 0,
   /* diffusers GEGLU after its projection (FeedForward, attention.py:190,259): kernel 1, no residual;
-   * w/bias rows interleaved per 160-row tile as [80 value rows, the 80 matching gate rows]; y is
-   * (batch*in_h*in_w, cout/2) = value * gelu(gate), rounded like K9. */
+   * w/bias rows interleaved per 16 rows as [8 value rows, the 8 matching gate rows] (ABI 13; was per
+   * 160); y is (batch*in_h*in_w, cout/2) = value * gelu(gate), rounded like K9. */
   VP2P_CONV_EPI_GEGLU = 1
 };
 

@@ -161,9 +161,9 @@ __device__ __forceinline__ float erf_fast(float x) {
 }
 
 // EPI = 0: bf16 output (+ residual).  EPI = 1 (GEGLU, 1x1 only): the weight rows come interleaved
-// per 160-column tile as [80 "a" rows, the 80 matching "gate" rows], and the epilogue writes
-// y[p, nt*80 + j] = a * gelu(g) (exact erf, each step rounded to bf16 as torch's eager GEGLU does)
-// into a (M, cout/2) output.  EPI = 2: split-K slice, fp32 accumulators to workspace[split].
+// per 16 as [8 "a" rows, the 8 matching "gate" rows], and the epilogue writes
+// y[p, (col / 16) * 8 + col % 8] = a * gelu(g) (erf to 1.8e-6, each step rounded to bf16 as torch's
+// eager GEGLU does) into a (M, cout/2) output from the accumulators.  EPI = 2: split-K slice, fp32 accumulators to workspace[split].
 // AM (addressing): 1 = 32-bit buffer offsets precomputed per DMA row (input below 2^31 bytes): the
 // per-step address is one add + the padding mask; 2 = the same with the x2 nearest upsample read on
 // the fly (per row: the source pixel's offset and the output pixel's parities; a tap's source row /
@@ -172,7 +172,6 @@ __device__ __forceinline__ float erf_fast(float x) {
 template <int KS, int EPI, int AM, int CF>
 __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   using Cfg = GCfg<CF>;
-  static_assert(EPI != 1 || Cfg::TBN % 160 == 0, "GEGLU interleave is per 160-column block");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w / Cfg::WCOL, wn = w - (w / Cfg::WCOL) * Cfg::WCOL;
@@ -401,8 +400,45 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       }
     return;
   }
-  bf16* Cs = reinterpret_cast<bf16*>(smem);
   const bf16* bias = static_cast<const bf16*>(a.bias);
+  if constexpr (EPI == 1) {
+    // GEGLU straight from the accumulators (no LDS staging): the weight rows are interleaved per 16
+    // as [8 value | 8 gate], so lane l (tile column l & 15 < 8) holds a channel's values and lane
+    // l ^ 8 its gates, for the same four rows 4 * fq + e.  One DPP exchange (row_ror:8) per pair of
+    // rows gives lane l (value, gate) of rows e = 0, 1 and lane l ^ 8 those of rows e = 2, 3; each
+    // lane then forms two outputs -- the projection rounded to bf16, gelu rounded, the product rounded,
+    // exactly K9's order -- on packed FP32.
+#pragma clang fp contract(off)
+    constexpr float kAlpha = 0.70710678118654752440f;
+    const int half = a.cout / 2;
+    bf16* y = static_cast<bf16*>(a.y);
+    const bool isv = fr < 8;
+#pragma unroll
+    for (int j = 0; j < WTN; ++j) {
+      const int gcol = n0 + wn * 80 + 16 * j + fr;            // interleaved projection column
+      const float bv = bias ? (float)bias[gcol] : 0.f;
+      const int oc = (gcol >> 4) * 8 + (fr & 7);              // output channel
+#pragma unroll
+      for (int i = 0; i < Cfg::WTM; ++i) {
+        float h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = (float)(bf16)(acc[i][j][e] + bv);
+        const float sx = isv ? h[2] : h[0], sy = isv ? h[3] : h[1];
+        const float rx = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sx), 0x128, 0xf, 0xf, false));
+        const float ry = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sy), 0x128, 0xf, 0xf, false));
+        const f32x2v val = isv ? f32x2v{h[0], h[1]} : f32x2v{rx, ry};
+        const f32x2v g = isv ? f32x2v{rx, ry} : f32x2v{h[2], h[3]};
+        const f32x2v gl = g * 0.5f * (1.f + erf_fast2(g * kAlpha));
+        const f32x2v ge = {(float)(bf16)gl.x, (float)(bf16)gl.y};
+        const f32x2v o = val * ge;
+        const int p0 = m0 + wm * Cfg::WR + 16 * i + 4 * fq + (isv ? 0 : 2);
+        if (p0 < M) y[(int64_t)p0 * half + oc] = (bf16)o.x;
+        if (p0 + 1 < M) y[(int64_t)(p0 + 1) * half + oc] = (bf16)o.y;
+      }
+    }
+    return;
+  }
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
   const float al = a.alpha == 0.f ? 1.f : a.alpha;     // x 1.0f is exact: alpha-free callers unchanged
   const bf16* res = static_cast<const bf16*>(a.residual);
   bf16* y = static_cast<bf16*>(a.y);
@@ -424,33 +460,6 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   }
   __syncthreads();
   const int mp = m0 + pass * Cfg::EROWS;
-  if constexpr (EPI == 1) {
-#pragma clang fp contract(off)
-    constexpr float kAlpha = 0.70710678118654752440f;
-    const int half = a.cout / 2;
-    for (int c = tid; c < Cfg::EROWS * (Cfg::TBN / 16); c += Cfg::NT) {
-      const int row = c / (Cfg::TBN / 16), ch = c - row * (Cfg::TBN / 16);
-      const int p = mp + row;
-      if (p >= M) continue;
-      // 160-column block blk of the tile = [80 value | 80 gate] columns; its outputs are the
-      // 80 columns (nt * TBN / 160 + blk) * 80 + [0, 80) of y, i.e. nt * TBN / 2 + ch * 8 + [0, 8)
-      const int blk = ch / 10, cc = ch - blk * 10;
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + blk * 160 + cc * 8);
-      const bf16x8 gv = *reinterpret_cast<const bf16x8*>(Cs + row * Cfg::CROWV + blk * 160 + 80 + cc * 8);
-      bf16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {    // erf_fast's operations in pairs: bit-equal to the scalar form
-        const f32x2v g = {(float)gv[j], (float)gv[j + 1]};
-        const f32x2v gl = g * 0.5f * (1.f + erf_fast2(g * kAlpha));
-        const f32x2v ge = {(float)(bf16)gl.x, (float)(bf16)gl.y};
-        const f32x2v o = f32x2v{(float)av[j], (float)av[j + 1]} * ge;
-        v[j] = (bf16)o.x;
-        v[j + 1] = (bf16)o.y;
-      }
-      *reinterpret_cast<bf16x8*>(y + (int64_t)p * half + nt * (Cfg::TBN / 2) + ch * 8) = v;
-    }
-    continue;
-  }
   for (int c = tid; c < Cfg::EROWS * (Cfg::TBN / 8); c += Cfg::NT) {
     const int row = c / (Cfg::TBN / 8), ch = c - row * (Cfg::TBN / 8);
     const int p = mp + row;
@@ -560,7 +569,7 @@ static int launch_g(const vp2p_conv_args& a, dim3 grid, int am, hipStream_t s) {
 // Tile choice for one-pass launches (split-K launches always take CF 0).
 // CF 1 (256 x 160, 3 stages): measured (profiles/r03_k10_tile_ab.jsonl, bit-equal) to win only on the
 // long-K 1x1 GEMMs (M 131072, K 1280, N 320: 185.5 -> 170.2 us), 2-8 % slower on the 3x3 convs and
-// the K = 320 GEMM / GEGLU shapes.  CF 2 (256 x 320 wide): Cout % 320 == 0, no GEGLU, and enough
+// the K = 320 GEMM / GEGLU shapes.  CF 2 (256 x 320 wide): Cout % 320 == 0 and enough
 // tiles to give every CU one.  VP2P_CONV_TILE=128 | 256 | wide | deep | auto (default) -- A/B, read once.
 static int tile_mode() {
   static const int m = [] {

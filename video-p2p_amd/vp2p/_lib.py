@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1

@@ -721,15 +721,16 @@ CONV = ConvSelector()
 
 
 def geglu_interleave(weight: torch.Tensor, bias: Optional[torch.Tensor]):
-    """Row order K10's GEGLU epilogue expects: per 160-row tile, 80 value rows then the 80 matching
-    gate rows (GEGLU.proj is [value; gate], diffusers' ``chunk(2, dim=-1)``)."""
+    """Row order K10's GEGLU epilogue expects: per 16 rows, 8 value rows then the 8 matching gate rows
+    (GEGLU.proj is [value; gate], diffusers' ``chunk(2, dim=-1)``), so that the two halves of every
+    16-column MFMA output tile hold a channel's value and gate in lanes l and l ^ 8."""
     n2, k = weight.shape
     inner = n2 // 2
     if inner % 80:
         raise ValueError("GEGLU inner width must be a multiple of 80")
-    t = inner // 80
-    w = torch.stack([weight[:inner].reshape(t, 80, k), weight[inner:].reshape(t, 80, k)], 1).reshape(n2, k)
-    b = None if bias is None else torch.stack([bias[:inner].reshape(t, 80), bias[inner:].reshape(t, 80)], 1).reshape(n2)
+    t = inner // 8
+    w = torch.stack([weight[:inner].reshape(t, 8, k), weight[inner:].reshape(t, 8, k)], 1).reshape(n2, k)
+    b = None if bias is None else torch.stack([bias[:inner].reshape(t, 8), bias[inner:].reshape(t, 8)], 1).reshape(n2)
     return w.contiguous(), (None if b is None else b.contiguous())
 
 
