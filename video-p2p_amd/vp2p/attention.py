@@ -36,7 +36,9 @@ def _cat_weight(module: nn.Module, names, cache_attr: str) -> torch.Tensor:
     if hit is not None and hit[0] == key:
         return hit[1]
     cat = torch.cat([w.detach() for w in ws], 0).contiguous()
-    object.__setattr__(module, cache_attr, (key, cat))
+    # the entry holds the weights themselves: a replaced parameter cannot reuse their memory (and so
+    # their key) while the entry lives
+    object.__setattr__(module, cache_attr, (key, cat, tuple(ws)))
     return cat
 
 
@@ -144,9 +146,11 @@ def _context_kv(module, ctx: torch.Tensor, heads: int):
     in-place write bumps ``_version``) recomputes them.  The cache holds the context tensor itself, so
     its memory cannot be recycled under an equal key."""
     wkv = _cat_weight(module, ("to_k", "to_v"), "_wkv")
-    bkey = None if module.to_k.bias is None else (module.to_k.bias.data_ptr(), module.to_k.bias._version,
-                                                   module.to_v.bias.data_ptr(), module.to_v.bias._version)
-    key = (ctx.data_ptr(), tuple(ctx.shape), tuple(ctx.stride()), ctx.dtype, ctx._version, wkv.data_ptr(), bkey, heads)
+    # the parameters themselves (storage and version), not the concatenated copy, whose memory is
+    # recycled when the weights change
+    pkey = tuple((p.data_ptr(), p._version, p.dtype) for m in (module.to_k, module.to_v)
+                 for p in (m.weight, m.bias) if p is not None)
+    key = (ctx.data_ptr(), tuple(ctx.shape), tuple(ctx.stride()), ctx.dtype, ctx._version, pkey, heads)
     # a HIP graph records the projection itself; VP2P_CTX_CACHE=0 recomputes per call (A/B)
     capturing = torch.cuda.is_current_stream_capturing() or not _CTX_CACHE
     hit = getattr(module, "_ctx_kv", None)
@@ -156,8 +160,9 @@ def _context_kv(module, ctx: torch.Tensor, heads: int):
     Ck = module.to_k.weight.shape[0]
     k, v = kv[..., :Ck], kv[..., Ck:]
     ws = ops.cross_kv_prep(k, v, heads)
-    if not capturing:
-        object.__setattr__(module, "_ctx_kv", (key, ctx, k, v, ws))
+    if not capturing:     # held: ctx and the parameters (their memory cannot be recycled under the key)
+        params = tuple(p for m in (module.to_k, module.to_v) for p in (m.weight, m.bias) if p is not None)
+        object.__setattr__(module, "_ctx_kv", (key, ctx, k, v, ws, params))
     return k, v, ws
 
 

@@ -225,7 +225,8 @@ class GEGLU(nn.Module):
         hit = getattr(self, "_il", None)
         if hit is None or hit[0] != key:
             with torch.no_grad():
-                hit = (key, ops.geglu_interleave(w.detach(), None if b is None else b.detach()))
+                # held with the entry: the parameters' memory cannot be recycled under the key
+                hit = (key, ops.geglu_interleave(w.detach(), None if b is None else b.detach()), (w, b))
             object.__setattr__(self, "_il", hit)
         return hit[1]
 
@@ -533,7 +534,7 @@ class UNet3DConditionModel(nn.Module):
         if hit is None or hit[0] != key:
             w = torch.cat([r.time_emb_proj.weight.detach() for r in rs]).contiguous()
             b = torch.cat([r.time_emb_proj.bias.detach() for r in rs])
-            hit = (key, w, b)
+            hit = (key, w, b, tuple(ps))      # the parameters held: their memory keeps its key
             object.__setattr__(self, "_temb_cat", hit)
         out = F.linear(F.silu(emb), hit[1], hit[2])
         off = 0
