@@ -10,6 +10,8 @@
 // two >= f); cross-token scores are masked to -inf, so one 32x32x16 product serves G tokens.
 // The source prompt's probability fragments stay in registers and are fed straight to the edited
 // prompts' P.V products: the self-replace is free.
+#include <stdlib.h>
+
 #include "common.hpp"
 #include "vp2p.h"
 
@@ -38,15 +40,19 @@ struct TempCfg {
 // over blockIdx.y.  For d <= 80 the next prompt's Q, K and V rows are fetched while the current
 // prompt computes (and the first prompt's V with its Q and K), so each wave exposes one HBM
 // latency instead of two per prompt.
-template <typename T, int D>
-__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void temporal_attn_p2p_kernel(const vp2p_temporal_attn_args a, int lf) {
+// WPB waves per workgroup = WPB heads of the same token block.  WPB = 8 (every head of the SD
+// layers): a workgroup reads whole 2C-byte q / k / v rows and writes whole O rows, so no 128-byte line
+// is split between workgroups that run at different times (WPB = 4 splits each row's lines between
+// two), at the same 8 waves per CU.
+template <typename T, int D, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB, sizeof(T) == 2 ? 8 / WPB : 1) void temporal_attn_p2p_kernel(const vp2p_temporal_attn_args a, int lf) {
   using M = Mfma<T>;
   using C = TempCfg<T, D>;
   constexpr bool PF = C::KS <= 5;
   constexpr int VN = (C::CPR + 1) / 2;          // V vectors per lane (c = h, h + 2, ...)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
-  const int head = blockIdx.y * 4 + w;
+  const int head = blockIdx.y * WPB + w;
   if (head >= a.heads) return;
   T* Vs = reinterpret_cast<T*>(smem + w * C::WAVE_LDS);
   for (int i = l; i < C::WAVE_LDS / 16; i += 64) reinterpret_cast<u32x4*>(Vs)[i] = u32x4{0, 0, 0, 0};
@@ -379,6 +385,15 @@ static int launch_temporal_long(const vp2p_temporal_attn_args* a, hipStream_t s)
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
+// VP2P_K3_WPB=8: eight heads per workgroup (A/B; default four), read once
+static int k3_wpb() {
+  static const int w = [] {
+    const char* e = getenv("VP2P_K3_WPB");
+    return (e && e[0] == '8') ? 8 : 4;
+  }();
+  return w;
+}
+
 template <typename T, int D>
 static int launch_temporal(const vp2p_temporal_attn_args* a, hipStream_t s) {
   if (a->frames > 64) return launch_temporal_long<T, D, 4>(a, s);
@@ -391,8 +406,12 @@ static int launch_temporal(const vp2p_temporal_attn_args* a, hipStream_t s) {
   const int groups = p2p ? (a->cond_only ? 1 : 2) : a->batch;
   const int64_t nwg = (int64_t)groups * ((a->tokens + G - 1) / G);
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-  hipLaunchKernelGGL((temporal_attn_p2p_kernel<T, D>), dim3((unsigned)nwg, (unsigned)((a->heads + 3) / 4)), dim3(256),
-                     4 * C::WAVE_LDS, s, *a, lf);
+  if (a->heads % 8 == 0 && k3_wpb() == 8)
+    hipLaunchKernelGGL((temporal_attn_p2p_kernel<T, D, 8>), dim3((unsigned)nwg, (unsigned)(a->heads / 8)), dim3(512),
+                       8 * C::WAVE_LDS, s, *a, lf);
+  else
+    hipLaunchKernelGGL((temporal_attn_p2p_kernel<T, D, 4>), dim3((unsigned)nwg, (unsigned)((a->heads + 3) / 4)), dim3(256),
+                       4 * C::WAVE_LDS, s, *a, lf);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
