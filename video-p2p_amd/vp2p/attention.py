@@ -79,7 +79,10 @@ class CrossAttention(nn.Module):
 class FrameAttention(CrossAttention):
     """Sparse-causal frame attention with first-frame K/V (attention.py:273-329) on K1."""
 
-    def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, video_length=None):
+    def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, video_length=None,
+                residual=None):
+        """``residual``: return residual + attn(x) (the block's add, attention.py:247-252), the add in
+        the output projection's epilogue (inference only)."""
         if attention_mask is not None:
             raise NotImplementedError("FrameAttention: attention_mask (never passed by the UNet)")
         if encoder_hidden_states is not None:
@@ -117,7 +120,8 @@ class FrameAttention(CrossAttention):
             kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
                           None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
             out = autograd.SharedKVAttention.apply(q, kv, f, self.heads, self.scale)
-            return self.to_out[1](self.to_out[0](out))
+            y = self.to_out[1](self.to_out[0](out))
+            return y if residual is None else y + residual
         wkv = _cat_weight(self, ("to_k", "to_v"), "_wkv")
         bkv = None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias])
         if pending is not None:
@@ -131,6 +135,8 @@ class FrameAttention(CrossAttention):
         kv = ops.linear(x0, wkv, bkv)
         out = ops.frame_attention(q, kv[..., :C], kv[..., C:], f, self.heads, scale=self.scale,
                                   q_prescaled=True)
+        if residual is not None:
+            return _linear_out_add(self.to_out[0], out, residual)
         return self.to_out[1](_linear_out(self.to_out[0], out))
 
 
@@ -211,7 +217,8 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
             q = F.linear(x, module.to_q.weight, module.to_q.bias)
             kv = F.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
                           None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))
-            return to_out(autograd.SharedKVAttention.apply(q, kv, f, h, module.scale))
+            y = to_out(autograd.SharedKVAttention.apply(q, kv, f, h, module.scale))
+            return y if residual is None else y + residual
         q = ops.linear(x, module.to_q.weight, module.to_q.bias)
         k, v, kv_ws = _context_kv(module, ctx, h)
         call = controller.fused_begin(True, place, N, f) if (controller is not None and fused) else LayerCall()
@@ -233,6 +240,8 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
             out = _pv(module, attn, v.contiguous(), B, f)
         elif controller is not None:
             controller.fused_end(True, place, call, probs)
+        if residual is not None:
+            return _linear_out_add(to_out, out, residual)
         return _linear_out(to_out, out)
 
     # self attention on the hooked path = temporal attention (attn_temp)
@@ -297,6 +306,15 @@ def _linear_out(to_out, out):
     if isinstance(to_out, nn.Linear) and not torch.is_grad_enabled():
         return ops.linear(out, to_out.weight, to_out.bias)
     return to_out(out)
+
+
+def _linear_out_add(to_out, out, residual):
+    """residual + to_out(out) (the block's residual add, attention.py:247-262) at inference: the add
+    in K10's epilogue where the projection runs on K10 (``ops.linear_add``), the two roundings of
+    the reference (projection, then sum) either way."""
+    if isinstance(to_out, nn.Linear) and not torch.is_grad_enabled() and out.is_contiguous():
+        return ops.linear_add(out, to_out.weight, to_out.bias, residual)
+    return to_out(out) + residual
 
 
 def _out_proj(to_out, out, residual):

@@ -838,6 +838,24 @@ def linear_k10(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tenso
     return y
 
 
+def linear_add(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+               residual: torch.Tensor) -> torch.Tensor:
+    """residual + (x @ W^T + b) with the reference's two roundings (the projection, then the sum):
+    one K10 launch with the add in its epilogue where ``LINEAR`` puts the projection on K10,
+    otherwise the projection (``linear``) and a separate add."""
+    K, N = x.shape[-1], weight.shape[0]
+    M = x.numel() // max(K, 1)
+    if (linear_k10_ok(x, weight, bias) and LINEAR.use_k10(M, K, N) and residual.is_contiguous()
+            and residual.dtype == x.dtype and residual.shape[:-1] == x.shape[:-1] and residual.shape[-1] == N):
+        return linear_residual(x, weight, bias, residual)
+    return linear(x, weight, bias) + residual
+
+
+def linear_add_fused(M: int, K: int, N: int) -> bool:
+    """Whether ``linear_add`` runs as one K10 launch for this shape (a fixed table lookup)."""
+    return LINEAR.use_k10(M, K, N) and K % 64 == 0 and N % 160 == 0
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
            alpha: Optional[float] = None) -> torch.Tensor:
     """nn.Linear (``alpha``: alpha * (x @ W^T + b), one rounding -- the pre-scaled FrameAttention query).

@@ -68,6 +68,7 @@ def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
 
 _FUSE_ADD_LN = os.environ.get("VP2P_FUSE_ADD_LN", "1") != "0"     # A/B switches for experiments
 _FUSE_GEGLU = os.environ.get("VP2P_FUSE_GEGLU", "1") != "0"
+_FUSE_OUT_RES = os.environ.get("VP2P_FUSE_OUT_RES", "0") == "1"   # measured 0.4 % slower: opt-in
 
 
 def _add_ln(h: torch.Tensor, x: torch.Tensor, norm: nn.LayerNorm):
@@ -237,12 +238,15 @@ class FeedForward(nn.Module):
         inner = dim * mult
         self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(dropout), nn.Linear(inner, dim)])
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
+        """``residual``: residual + ff(x) (the block's add, attention.py:259), fused at inference."""
         x = self.net[1](self.net[0](x))
         out = self.net[2]
         if not torch.is_grad_enabled():
+            if residual is not None:
+                return ops.linear_add(x, out.weight, out.bias, residual)
             return ops.linear(x, out.weight, out.bias)
-        return out(x)
+        return out(x) if residual is None else out(x) + residual
 
 
 class BasicTransformerBlock(nn.Module):
@@ -266,13 +270,23 @@ class BasicTransformerBlock(nn.Module):
             x = self.ff(layer_norm(self.norm3, x)) + x
             x = self.attn_temp(layer_norm(self.norm_temp, x), video_length=frames, temporal_layout="bf") + x
             return x
-        # inference: each residual add is fused into the next LayerNorm (K8 + add), same roundings
-        h = self.attn1(layer_norm(self.norm1, x), video_length=frames)
-        x, y = _add_ln(h, x, self.norm2)
-        h = self.attn2(y, encoder_hidden_states=context, video_length=frames)
-        x, y = _add_ln(h, x, self.norm3)
-        h = self.ff(y)
-        x, y = _add_ln(h, x, self.norm_temp)
+        # inference: each residual add rides on the output projection's K10 epilogue where K10 runs
+        # that projection (the next LayerNorm then reads one tensor instead of two and writes one),
+        # otherwise on the next LayerNorm (K8 + add); the same two roundings either way
+        C = x.shape[-1]
+        M = x.numel() // C
+        if _FUSE_OUT_RES and x.is_contiguous() and ops.linear_add_fused(M, C, C) and ops.linear_add_fused(M, 4 * C, C):
+            x = self.attn1(layer_norm(self.norm1, x), video_length=frames, residual=x)
+            x = self.attn2(layer_norm(self.norm2, x), encoder_hidden_states=context, video_length=frames, residual=x)
+            x = self.ff(layer_norm(self.norm3, x), residual=x)
+            y = layer_norm(self.norm_temp, x)
+        else:
+            h = self.attn1(layer_norm(self.norm1, x), video_length=frames)
+            x, y = _add_ln(h, x, self.norm2)
+            h = self.attn2(y, encoder_hidden_states=context, video_length=frames)
+            x, y = _add_ln(h, x, self.norm3)
+            h = self.ff(y)
+            x, y = _add_ln(h, x, self.norm_temp)
         # the last residual add rides on attn_temp's output projection (fused where it measures faster)
         return self.attn_temp(y, video_length=frames, temporal_layout="bf", residual=x)
 
