@@ -39,7 +39,7 @@ def _cpu_worker(rank, world, port, out_path):
     dist = _init(rank, world, port)
     from vp2p.frame_parallel import FrameShard
     torch.manual_seed(0)
-    B, f, N, C = 3, 4, 8, 6
+    B, f, N, C = 3, 4, 16, 6
     full = torch.randn(B * f, N, C)                                  # '(b f) n c', identical on all ranks
     sh = FrameShard()
     loc = full.reshape(B, f, N, C)[:, rank * (f // world):(rank + 1) * (f // world)].reshape(-1, N, C)
@@ -57,6 +57,14 @@ def _cpu_worker(rank, world, port, out_path):
     ok.append(torch.equal(sh.gather(sh.local(lat, 2), 2), lat))
     flat = torch.arange(5, dtype=torch.float32) + 10 * rank
     ok.append(torch.equal(sh.all_gather_flat(flat), torch.cat([torch.arange(5.0) + 10 * r for r in range(world)])))
+    # attn_temp's exchange: the hidden state crosses, fn (per token, mixing all frames, C -> 2C) runs
+    # on the token slice, in 1, 2 or 4 pieces; equals fn on the whole clip, this rank's frames
+    wmix = torch.randn(C, 2 * C, generator=torch.Generator().manual_seed(3))
+    fn = lambda t: torch.cumsum(t.reshape(B, f, t.shape[1], C), 1).reshape(B * f, t.shape[1], C) @ wmix
+    want_t = fn(full).reshape(B, f, N, 2 * C)[:, rank * (f // world):(rank + 1) * (f // world)].reshape(-1, N, 2 * C)
+    for chunks in (1, 2, 4):
+        got_t = sh.temporal_exchange(loc.contiguous(), B, fn, chunks)
+        ok.append(bool(torch.allclose(got_t, want_t, atol=1e-5)))
     torch.save(ok, out_path + f".{rank}")
     dist.destroy_process_group()
 

@@ -30,43 +30,9 @@
 
 #include <type_traits>
 
-#include "common.hpp"
-#include "vp2p.h"
+#include "frame_attn.hpp"
 
 namespace vp2p {
-
-constexpr float kRescaleThr = 8.0f;
-
-template <typename T, int D>
-struct FrameCfg {
-  static constexpr bool BF = sizeof(T) == 2;
-  static constexpr int KD = Mfma<T>::KD;
-  static constexpr int DP = round_up(D, KD);
-  static constexpr int KS = DP / KD;
-  static constexpr int DV = round_up(D, 32);
-  static constexpr int NT = DV / 32;
-  static constexpr bool ONES = D < DV;                           // spare V^T row carries the row sum
-  static constexpr int KT = (BF && D <= 80) ? 128 : 64;          // keys per LDS tile
-  static constexpr int NB = D <= 80 ? 2 : 1;                     // 32-key score blocks in flight
-  static constexpr int SUBK = 32 * NB;
-  static constexpr int EPC = 16 / (int)sizeof(T);                // elements per 16-byte chunk
-  static constexpr int CPR = D / EPC;                            // chunks per K/V row
-  static constexpr int NCH = (KT * CPR + 255) / 256;             // chunks per thread per tile
-  // bf16: K rows read with ds_read_b128 by 16-lane groups -> stride = 4 (mod 8) dwords;
-  //       V rows read with ds_read_b64_tr_b16 -> stride = 16 or 48 (mod 64) dwords.
-  // f32 : K read one dword per lane down a column -> odd stride; V read along rows.
-  static constexpr int vrow_bf16() {
-    int v = DV;
-    while (!((v / 2) % 64 == 16 || (v / 2) % 64 == 48)) v += 8;
-    return v;
-  }
-  static constexpr int KROW = BF ? DP + 8 : DP + 1;
-  static constexpr int VROW = BF ? vrow_bf16() : DV;
-  static constexpr int LDS_BYTES = (KT * KROW + KT * VROW) * (int)sizeof(T);
-  // accumulator slot of O^T row D (the ones row): tile, register, lane half
-  static constexpr int ONE_T = D / 32, ONE_L = D % 32;
-  static constexpr int ONE_H = (ONE_L >> 2) & 1, ONE_I = (ONE_L & 3) + 4 * (ONE_L >> 3);
-};
 
 template <typename T, int D>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel(const vp2p_frame_attn_args a) {
@@ -283,48 +249,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
 //  * with no branch inside a tile, QK^T of block j+1 is issued before the exp2/cvt of block j, so
 //    the VALU softmax of one block runs under the MFMAs of the next (T15 "att[2]").
 // ------------------------------------------------------------------------------------------------
-constexpr float kSumThr = 4096.f;
-
-
-// Exact two-pass softmax row of one query in plain fp32 VALU (the overflow fallback of x2f):
-// writes this lane's epilogue slots of the output row and the row's log-sum-exp.
-// Small register footprint (the query row is re-read from memory, one 4-column output slot
-// accumulated at a time) so this rare path does not add to the kernel's register budget.
-template <int D>
-__device__ __forceinline__ void frame_attn_exact_row(const vp2p_frame_attn_args& a, int b, int head, int fr,
-                                                     int pos, int64_t qi, int h, float cs) {
-  const bf16* qrow = static_cast<const bf16*>(a.q) + b * a.q_sb + (int64_t)fr * a.q_sf + (int64_t)pos * a.q_sn + head * D;
-  const bf16* kb = static_cast<const bf16*>(a.k) + b * a.k_sb + head * D;
-  const bf16* vb = static_cast<const bf16*>(a.v) + b * a.v_sb + head * D;
-  auto score = [&](int key) {
-    const bf16* kr = kb + (int64_t)key * a.k_sn;
-    float s = 0.f;
-    for (int c = 0; c < D; ++c) s = __builtin_fmaf((float)qrow[c], (float)kr[c], s);
-    return s;
-  };
-  float mx = kNegInf;
-  for (int key = 0; key < a.tokens_kv; ++key) mx = fmaxf(mx, score(key) * cs);
-  float l = 0.f;
-  for (int key = 0; key < a.tokens_kv; ++key) l += exp2f(__builtin_fmaf(score(key), cs, -mx));
-  const int FQ = a.frames * a.tokens_q;
-  if (a.lse) a.lse[(int64_t)(b * a.heads + head) * FQ + qi] = mx + log2f(l);
-  const float inv = 1.f / l;
-  bf16* orow = static_cast<bf16*>(a.o) + b * a.o_sb + (int64_t)fr * a.o_sf + (int64_t)pos * a.o_sn + head * D;
-  for (int dc = 4 * h; dc < D; dc += 8) {        // this lane's 4-column slots of each 8-column group
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int key = 0; key < a.tokens_kv; ++key) {
-      const float p = exp2f(__builtin_fmaf(score(key), cs, -mx));
-      const bf16* vr = vb + (int64_t)key * a.v_sn + dc;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = __builtin_fmaf(p, (float)vr[j], acc[j]);
-    }
-    bf16x4 v;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (bf16)(acc[j] * inv);
-    *reinterpret_cast<bf16x4*>(orow + dc) = v;
-  }
-}
-
 // Two forms of the inner loop:
 //   FOLD = false: p = exp2(s * c - m) (c = scale * log2 e): one v_fma + one v_exp + half a v_cvt per
 //                 score; set 0's QK^T then set 1's, then the two softmax + PV halves;
@@ -675,6 +599,10 @@ static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
     constexpr int KT = D <= 64 ? 256 : 64;
     const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
     if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+#if VP2P_K1_PP
+    if constexpr (D == 40)
+      if (a->q_prescaled && a->tokens_kv % 128 == 0) return launch_frame_attn_pp(a, stream);
+#endif
     if constexpr (C::DP > D)
       if (a->q_prescaled) return launch_x2f<D, 128, true>(a, nwg, stream);
     return launch_x2f<D, KT, false>(a, nwg, stream);

@@ -1,0 +1,444 @@
+// K1 at res-64 -- FrameAttention with first-frame K/V (tuneavideo/models/attention.py:282-322) in
+// the form the UNet calls it there: bf16, head_dim 40, q pre-scaled by scale * log2(e) (the to_q
+// GEMM's alpha), tokens_kv a multiple of 128.  These launches carry 88 % of K1's FLOPs.
+//
+// Why a separate kernel: at d = 40 a 32x32 score block is 7 MFMAs (3 QK^T k-steps, 4 PV) against
+// 16 v_exp + 8 v_cvt per lane, so the SIMD's issue port -- not the matrix pipe -- is the tight
+// resource, and the compiler-scheduled x2f loop (frame_attn.hip) keeps each block's exps waiting on
+// that block's own QK^T MFMAs (its 8-exp bursts leave the matrix pipe idle).  Here one wave per SIMD
+// runs SETS independent 32-query sets as one software pipeline over the whole key axis, with the
+// instruction order written out slot by slot:
+//  * an iteration (one 32-key block) is SETS groups of 7 MFMA slots; group g issues PV of set g's
+//    previous block (4 MFMAs) and QK^T of the set whose exps the previous group finished (3 MFMAs),
+//    and beside those 7 MFMAs the 16 v_exp + 8 v_cvt of set g: 2-3 exps and about one cvt per MFMA
+//    gap (CDNA guide T19 / MI355X_MICROARCH 'vector-instruction ISSUE cost'), nothing waiting on an
+//    MFMA of the same group;
+//  * O^T lives in the accumulator file (AGPRs), written only by the PV MFMAs (inline asm, so hipcc
+//    keeps it there); scores, P, Q and the K/V fragments fit the arch VGPRs;
+//  * each K / V^T fragment is re-read as soon as its last MFMA of the block has issued, >= 5 MFMA
+//    slots before its next use;
+//  * K and V tiles of 128 keys arrive by LDS-DMA (buffer_load ... lds, 32-bit offsets, no register
+//    staging) in dense 80-byte rows, through a 3-slot ring with ONE barrier per tile: tile t+2 is
+//    issued right after tile t's barrier, the first point where every wave is done with tile t-1;
+//  * the padding the MFMAs need is never stored: the K fragment of columns 40..47 (the folded -m
+//    column: Q'[40] = -m, K[40] = 1) and V^T rows 40..63 (row 40 all ones = the row sum) are read by
+//    the lanes that own them from 16 replicas of one 16-byte constant, placed where the fragment
+//    reads' immediate offsets land (broadcast reads, no per-read select);
+//  * the row-sum growth check of x2f runs once per tile; when it moves m it also rescales the work
+//    still in flight (every set's packed P, the next block's scores), so every term enters O at one
+//    scale (CDNA guide T13 hazard).
+#include "frame_attn.hpp"
+
+#ifndef VP2P_K1_PP_SETS
+#define VP2P_K1_PP_SETS 4
+#endif
+
+namespace vp2p {
+
+namespace {
+
+typedef __attribute__((address_space(3))) char lchar;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kD = 40, kKT = 128, kRowB = kD * 2;                 // dense K / V rows: 80 bytes
+constexpr int kSlotB = kKT * kRowB;                               // 10 KiB per K or V slot
+constexpr int kNSlot = 3;
+constexpr int kChunks = kKT * kD / 8;                             // 16-byte chunks per tile: 640
+constexpr int kDmaPerTile = kChunks / 64;                          // wave-instructions per tile: 10
+static_assert(kChunks % 64 == 0, "whole DMA instructions");
+// LDS: K ring, V ring, constant replicas [1, 0 x 7] at kCR + 64 + 640 k (k = 0..15)
+constexpr int kKRing = 0, kVRing = kNSlot * kSlotB, kCR = 2 * kNSlot * kSlotB;
+constexpr int kLdsBytes = kCR + 64 + 640 * 15 + 16;
+
+__device__ __forceinline__ bf16x8 ld128(const lchar* p) { return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(p); }
+__device__ __forceinline__ bf16x4 ldtr(const lchar* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(p));
+}
+// The inner loop is written out instruction by instruction: every MFMA, v_exp and v_cvt of it is a
+// volatile asm statement, so neither the IR passes nor the machine scheduler can move one (hipcc
+// otherwise clusters the exps in bursts of 8-40 between MFMAs).  Only the LDS reads, their waits
+// and the address arithmetic are left to the compiler.  Hazards the compiler cannot see are excluded
+// by the slot order (kernel header):
+//  * v_exp (trans) -> v_cvt reading it: an MFMA sits between them (a slot is cvts, exps, MFMA);
+//  * v_cvt -> PV MFMA reading the packed P: one whole block apart;
+//  * QK^T MFMA -> v_exp reading the scores: >= 9 MFMA slots apart;
+//  * VALU write of P / O / Q' in the rare rescale -> MFMA: the s_nop 1 opening every block;
+//  * PV MFMA -> VALU read of O: o_fence() (two s_nop 7).
+__device__ __forceinline__ float vexp(float x) {
+  float y;
+  asm volatile("v_exp_f32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+__device__ __forceinline__ uint32_t vcvt(float x, float y) {
+  uint32_t r;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+// S^T = K . Q'^T, three k-steps; the chain's first step starts from 0
+__device__ __forceinline__ void qk_first(f32x16& acc, const bf16x8& k, const bf16x8& q) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(k), "v"(q));
+}
+__device__ __forceinline__ void qk_next(f32x16& acc, const bf16x8& k, const bf16x8& q) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(k), "v"(q));
+}
+__device__ __forceinline__ void sb() { __builtin_amdgcn_sched_barrier(0); }
+
+// O^T += V^T . P^T into an accumulator-file tile (O stays in AGPRs).
+__device__ __forceinline__ void pv(f32x16& o, const bf16x8& v, const u32x4& p) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(__builtin_bit_cast(bf16x8, p)));
+}
+
+// the slot-6 PV with the block's last bf16 packing behind it in the same statement
+__device__ __forceinline__ void pv_cvt(f32x16& o, const bf16x8& v, const u32x4& p, uint32_t& pk, float x, float y) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %3, %0\n\tv_cvt_pk_bf16_f32 %1, %4, %5"
+               : "+a"(o), "=&v"(pk) : "v"(v), "v"(__builtin_bit_cast(bf16x8, p)), "v"(x), "v"(y));
+}
+
+}  // namespace
+
+template <int SETS>
+__global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_attn_args a) {
+  static_assert(SETS >= 2, "the QK^T of the last set rides in group 0 of the next block");
+  using T = bf16;
+  using M = Mfma<T>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  lchar* const L = (lchar*)smem;
+
+  const int tid = threadIdx.x, l = tid & 63, r = l & 31, h = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int QW = 32 * SETS, QB = 4 * QW;
+  const int FQ = a.frames * a.tokens_q;
+  const int qblocks = (FQ + QB - 1) / QB;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = bid / qblocks, qb = bid - bh * qblocks;
+  const int b = bh / a.heads, head = bh - b * a.heads;
+  const int Nk = a.tokens_kv;
+  const int ntiles = Nk / kKT;
+
+  // queries: SETS sets of 32 per wave; Q'[40] (lane half 1, k-step 2, element 0) carries -m
+  auto qrow_of = [&](int st, int& qi, int& fr, int& pos) {
+    qi = qb * QB + w * QW + st * 32 + r;
+    const bool v = qi < FQ;
+    fr = v ? qi / a.tokens_q : 0;
+    pos = v ? qi - fr * a.tokens_q : 0;
+    return v;
+  };
+  bf16x8 qf[SETS][3];
+#pragma unroll
+  for (int st = 0; st < SETS; ++st) {
+    int qi, fr, pos;
+    const bool qv = qrow_of(st, qi, fr, pos);
+    const T* qrow = static_cast<const T*>(a.q) + b * a.q_sb + fr * a.q_sf + pos * a.q_sn + head * kD;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) qf[st][s] = qv ? M::row_frag(qrow, s, h, kD) : M::zero();
+  }
+
+  // K / V tile DMA: wave w issues instructions n = w, w + 4, w + 8 (< 10) of each tile; lane l of
+  // instruction n moves chunk 64n + l = (row, chunk-in-row) of the dense image
+  const T* kb_ = static_cast<const T*>(a.k) + b * a.k_sb + head * kD;
+  const T* vb_ = static_cast<const T*>(a.v) + b * a.v_sb + head * kD;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>(kb_), 0, (uint32_t)((int64_t)(Nk - 1) * a.k_sn * 2 + kRowB), 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>(vb_), 0, (uint32_t)((int64_t)(Nk - 1) * a.v_sn * 2 + kRowB), 0x00020000);
+  constexpr int NDMA = (kDmaPerTile + 3) / 4;
+  uint32_t kvo[NDMA], vvo[NDMA];
+#pragma unroll
+  for (int i = 0; i < NDMA; ++i) {
+    const int c = 64 * (w + 4 * i) + l, row = c / 5, ch = c - row * 5;
+    kvo[i] = (uint32_t)(row * a.k_sn * 2 + ch * 16);
+    vvo[i] = (uint32_t)(row * a.v_sn * 2 + ch * 16);
+  }
+  const uint32_t k_tile_b = (uint32_t)(kKT * a.k_sn * 2), v_tile_b = (uint32_t)(kKT * a.v_sn * 2);
+  // The DMA is inline asm: hipcc would otherwise treat every later LDS read as dependent on it and
+  // drain vmcnt to 0 before the first one.  Its completion is waited for explicitly (vmcnt(0) before
+  // the barrier that publishes the tile).
+  const uint32_t lds_base = (uint32_t)(uintptr_t)L;
+  auto dma_tile = [&](int t) {
+    const int tt = min(t, ntiles - 1);     // past the end: reload the last tile into a dead slot
+    const int slot = t % kNSlot;
+    const uint32_t ks = (uint32_t)tt * k_tile_b, vs = (uint32_t)tt * v_tile_b;
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int n = w + 4 * i;
+      if (i + 1 < NDMA || n < kDmaPerTile) {
+        const uint32_t kd = __builtin_amdgcn_readfirstlane(lds_base + kKRing + slot * kSlotB + n * 1024);
+        const uint32_t vd = __builtin_amdgcn_readfirstlane(lds_base + kVRing + slot * kSlotB + n * 1024);
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                     :: "v"(kvo[i]), "s"(krs), "s"(kd), "s"(ks) : "memory");
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                     :: "v"(vvo[i]), "s"(vrs), "s"(vd), "s"(vs) : "memory");
+      }
+    }
+  };
+
+  // constant replicas, then tiles 0 and 1
+  if (tid < 16) {
+    u32x4 c1 = {__builtin_bit_cast(uint16_t, (T)1.0f), 0u, 0u, 0u};
+    *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(L + kCR + 64 + 640 * tid) = c1;
+  }
+  dma_tile(0);
+  dma_tile(1);
+
+  // per-lane LDS read bases (the slot is added per tile)
+  //  K fragment (row r, chunk 2si + h); k-step 2 of lane half 1 reads the fold constant
+  const int k_lane = r * kRowB + 16 * h;
+  //  V^T fragment (vt_frag_lds geometry): lane (h, g, q, p) reads row 4h + q (+8 for the high half)
+  //  of a 16-key step, columns 16g + 4p of tile t; tile 1's columns >= 40 are the constants
+  const int vg = (l >> 4) & 1, q4 = (l >> 2) & 3, p4 = l & 3;
+  const int v_lane = (4 * h + q4) * kRowB + 2 * (16 * vg + 4 * p4);
+  const bool v1c = vg == 1 || p4 >= 2;
+  const lchar* const v1const = L + kCR + ((vg == 0 && p4 == 2) ? 0 : 8);
+
+  float m[SETS], lp[SETS];
+  f32x16 o[SETS][2];
+  f32x16 S[SETS];
+  u32x4 P[SETS][2];
+#pragma unroll
+  for (int st = 0; st < SETS; ++st) {
+    lp[st] = 0.f;
+    o[st][0] = zero16();
+    o[st][1] = zero16();
+    P[st][0] = u32x4{0, 0, 0, 0};
+    P[st][1] = u32x4{0, 0, 0, 0};
+  }
+  auto set_negm = [&](int st) {
+    const bf16 nm = (bf16)(-m[st]);
+    if (h == 1) qf[st][2][0] = nm;
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  bf16x8 kf[3], vf[2][2];
+  // m starts at the exact row max of keys 0..31 (fold slot still 0: S = q'.k)
+  {
+    const lchar* kb0 = L + kKRing + k_lane;
+    kf[0] = ld128(kb0);
+    kf[1] = ld128(kb0 + 32);
+    kf[2] = ld128((h ? L + kCR : kb0) + 64);
+#pragma unroll
+    for (int st = 0; st < SETS; ++st) {
+      f32x16 s = M::mma(kf[0], qf[st][0], zero16());
+      s = M::mma(kf[1], qf[st][1], s);
+      s = M::mma(kf[2], qf[st][2], s);
+      float v = s[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) v = fmaxf(v, s[i]);
+      m[st] = (float)(bf16)fmaxf(v, xhalf(v));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] -= m[st];
+      S[st] = s;
+      set_negm(st);
+    }
+    // V "block -1" for the first PVs (P = 0: any finite data)
+    const lchar* vb0 = L + kVRing + v_lane;
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) vf[sp][t] = ld128(vb0);
+  }
+
+  // One block (iteration j).  On entry: S[g] = block j scores of sets 0..SETS-2 (at -m), S[SETS-1]
+  // dead (its block j QK^T rides in group 0 here); P = block j-1 packed; kf = K block j; vf = V^T
+  // block j-1.  Group 0 replaces kf by K block j+1 as its QK^T k-steps retire each fragment; the last
+  // group replaces vf by V^T block j as its PVs retire each fragment.
+  auto block = [&](const lchar* kb, const lchar* k2b, int krow, const lchar* vb, const lchar* v1b, int vrow) {
+    sb();
+    asm volatile("s_nop 1");
+    auto v_tr = [&](int sp, int t) {
+      const int rb = (vrow + 16 * sp) * kRowB + (t ? 64 : 0);
+      const lchar* p = t ? v1b : vb;
+      const bf16x4 lo = ldtr(p + rb), hi = ldtr(p + rb + 8 * kRowB);
+      bf16x8 f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { f[j] = lo[j]; f[4 + j] = hi[j]; }
+      return f;
+    };
+#pragma unroll
+    for (int g = 0; g < SETS; ++g) {
+      const int qs = (g + SETS - 1) % SETS;                     // whose QK^T rides in this group
+      const bool last = g == SETS - 1;
+      float e[16];
+      uint32_t pn[8];
+      f32x16 acc;
+      const f32x16& sg = S[g];
+      // slot 0: exps 0-2 | PV(sp 0, tile 1)
+      e[0] = vexp(sg[0]); e[1] = vexp(sg[1]); e[2] = vexp(sg[2]);
+      pv(o[g][1], vf[0][1], P[g][0]);
+      if (last) vf[0][1] = v_tr(0, 1);
+      sb();
+      // slot 1: cvt 0-1, exps 3-4 | QK k-step 0
+      pn[0] = vcvt(e[0], e[1]);
+      e[3] = vexp(sg[3]); e[4] = vexp(sg[4]);
+      qk_first(acc, kf[0], qf[qs][0]);
+      if (g == 0) kf[0] = ld128(kb + krow * kRowB);
+      sb();
+      // slot 2: cvt 2-3, exps 5-6 | PV(sp 0, tile 0)
+      pn[1] = vcvt(e[2], e[3]);
+      e[5] = vexp(sg[5]); e[6] = vexp(sg[6]);
+      pv(o[g][0], vf[0][0], P[g][0]);
+      if (last) vf[0][0] = v_tr(0, 0);
+      sb();
+      // slot 3: cvt 4-5, exps 7-8 | QK k-step 1
+      pn[2] = vcvt(e[4], e[5]);
+      e[7] = vexp(sg[7]); e[8] = vexp(sg[8]);
+      qk_next(acc, kf[1], qf[qs][1]);
+      if (g == 0) kf[1] = ld128(kb + krow * kRowB + 32);
+      sb();
+      // slot 4: cvt 6-7, exps 9-10 | PV(sp 1, tile 1)
+      pn[3] = vcvt(e[6], e[7]);
+      e[9] = vexp(sg[9]); e[10] = vexp(sg[10]);
+      pv(o[g][1], vf[1][1], P[g][1]);
+      if (last) vf[1][1] = v_tr(1, 1);
+      sb();
+      // slot 5: cvt 8-9, exps 11-13 | QK k-step 2 -> S[qs]
+      pn[4] = vcvt(e[8], e[9]);
+      e[11] = vexp(sg[11]); e[12] = vexp(sg[12]); e[13] = vexp(sg[13]);
+      qk_next(acc, kf[2], qf[qs][2]);
+      if (g == 0) kf[2] = ld128(k2b + krow * kRowB + 64);
+      sb();
+      // slot 6: cvt 10-13, exps 14-15 | PV(sp 1, tile 0), cvt 14-15 (same statement: the MFMA
+      // separates the trans write of e15 from its read)
+      pn[5] = vcvt(e[10], e[11]);
+      pn[6] = vcvt(e[12], e[13]);
+      e[14] = vexp(sg[14]); e[15] = vexp(sg[15]);
+      pv_cvt(o[g][0], vf[1][0], P[g][1], pn[7], e[14], e[15]);
+      if (last) vf[1][0] = v_tr(1, 0);
+      S[qs] = acc;
+      P[g][0] = u32x4{pn[0], pn[1], pn[2], pn[3]};
+      P[g][1] = u32x4{pn[4], pn[5], pn[6], pn[7]};
+      sb();
+    }
+  };
+  // O reads by the VALU: past the last PV MFMA's write (>= 12 wait states for this 8-pass MFMA)
+  auto o_fence = [&]() {
+#pragma unroll
+    for (int st = 0; st < SETS; ++st) asm volatile("s_nop 7\n\ts_nop 7" : "+a"(o[st][0]), "+a"(o[st][1]));
+  };
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int s0 = (t % kNSlot) * kSlotB, s1 = ((t + 1) % kNSlot) * kSlotB;
+    // per-tile bases, opaque so hipcc folds the block offsets into the reads' immediates instead of
+    // hoisting one address register per read out of the loop
+    const lchar* kb0 = L + kKRing + s0 + k_lane;
+    const lchar* kb1 = L + kKRing + s1 + k_lane;
+    const lchar* vb = L + kVRing + s0 + v_lane;
+    asm volatile("" : "+v"(kb0), "+v"(kb1), "+v"(vb));
+    const lchar* k2b0 = h ? L + kCR : kb0;
+    const lchar* k2b1 = h ? L + kCR : kb1;
+    const lchar* v1b = v1c ? v1const : vb;
+    asm volatile("" : "+v"(k2b0), "+v"(k2b1), "+v"(v1b));
+    block(kb0, k2b0, 32, vb, v1b, 0);
+    // tile t+1 (issued a tile ago) has landed; every wave is done with tile t-1's slot (K last read
+    // in iteration 4t-2, V in 4t-1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    dma_tile(t + 2);
+    block(kb0, k2b0, 64, vb, v1b, 32);
+    block(kb0, k2b0, 96, vb, v1b, 64);
+    block(kb1, k2b1, 0, vb, v1b, 96);
+    // once per tile: the row-sum growth check.  O holds blocks <= 4t+2; P (block 4t+3) and
+    // S[0..SETS-2] (block 4t+4) are still at the old m; S[SETS-1] is recomputed with the new fold.
+    sb();
+    o_fence();
+    float lc[SETS];
+    bool grow = false;
+#pragma unroll
+    for (int st = 0; st < SETS; ++st) {
+      lc[st] = o[st][1][4];             // O^T row 40 (lanes h == 0; the other half reads a zero row)
+      grow |= lc[st] - lp[st] > kSumThr;
+    }
+    if (__any(grow)) {
+#pragma unroll
+      for (int st = 0; st < SETS; ++st) {
+        const float mine = lc[st] - lp[st];
+        const float other = xhalf(mine);
+        const float dl = h == 0 ? mine : other;
+        const float mn = dl > kSumThr ? (float)(bf16)(m[st] + __log2f(dl)) : m[st];
+        const float alpha = fast_exp2(m[st] - mn);
+        const float shift = m[st] - mn;
+        m[st] = mn;
+        set_negm(st);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          o[st][0][i] *= alpha;
+          o[st][1][i] *= alpha;
+          S[st][i] += shift;
+        }
+        lc[st] *= alpha;
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          bf16x8 pp = __builtin_bit_cast(bf16x8, P[st][sp]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pp[j] = (bf16)((float)pp[j] * alpha);
+          P[st][sp] = __builtin_bit_cast(u32x4, pp);
+        }
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < SETS; ++st) lp[st] = lc[st];
+  }
+  // drain: PV of the last block
+  sb();
+  asm volatile("s_nop 1");
+#pragma unroll
+  for (int st = 0; st < SETS; ++st) {
+    pv(o[st][1], vf[0][1], P[st][0]);
+    pv(o[st][0], vf[0][0], P[st][0]);
+    pv(o[st][1], vf[1][1], P[st][1]);
+    pv(o[st][0], vf[1][0], P[st][1]);
+  }
+  o_fence();
+
+#pragma unroll
+  for (int st = 0; st < SETS; ++st) {
+    int qi_, fr_, pos_;
+    const bool qv_ = qrow_of(st, qi_, fr_, pos_);
+    const float mine = o[st][1][4];
+    const float other = xhalf(mine);
+    const float lrow = h == 0 ? mine : other;
+    bool bad = qv_ && (__float_as_uint(lrow) & 0x7f800000u) == 0x7f800000u;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bad |= qv_ && (__float_as_uint(o[st][t][i]) & 0x7f800000u) == 0x7f800000u;
+    if (qv_ && !bad) {
+      if (a.lse) a.lse[(int64_t)(b * a.heads + head) * FQ + qi_] = m[st] + log2f(lrow);
+      const float inv = 1.f / lrow;
+      T* orow = static_cast<T*>(a.o) + b * a.o_sb + fr_ * a.o_sf + pos_ * a.o_sn + head * kD;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int dc = 32 * t + 8 * gg + 4 * h;
+          if (dc < kD) {
+            bf16x4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[st][t][4 * gg + j] * inv);
+            *reinterpret_cast<bf16x4*>(orow + dc) = v;
+          }
+        }
+    }
+    if (bad) frame_attn_exact_row<kD>(a, b, head, fr_, pos_, qi_, h, 1.f);
+  }
+}
+
+int launch_frame_attn_pp(const vp2p_frame_attn_args* a, hipStream_t stream) {
+  constexpr int SETS = VP2P_K1_PP_SETS;
+  if (a->dtype != VP2P_BF16 || a->head_dim != kD || !a->q_prescaled || a->tokens_kv % kKT) return VP2P_E_SHAPE;
+  // 32-bit buffer offsets: every key row of one (b, head) within 4 GiB
+  if ((int64_t)a->tokens_kv * a->k_sn * 2 >= (1ll << 32) || (int64_t)a->tokens_kv * a->v_sn * 2 >= (1ll << 32))
+    return VP2P_E_SHAPE;
+  const int FQ = a->frames * a->tokens_q;
+  const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 128 * SETS - 1) / (128 * SETS));
+  if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_pp<SETS>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) == hipSuccess;
+  if (!attr) return VP2P_E_LAUNCH;
+  hipLaunchKernelGGL((frame_attn_kernel_pp<SETS>), dim3((unsigned)nwg), dim3(256), kLdsBytes, stream, *a);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+}  // namespace vp2p

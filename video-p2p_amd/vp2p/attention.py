@@ -31,11 +31,13 @@ from .controllers import LayerCall
 
 def _cat_weight(module: nn.Module, names, cache_attr: str) -> torch.Tensor:
     ws = [getattr(module, n).weight for n in names]
-    key = tuple((w.data_ptr(), w._version, w.dtype, w.device) for w in ws)
+    key = ops.version_key(*ws)
     hit = getattr(module, cache_attr, None)
-    if hit is not None and hit[0] == key:
+    if hit is not None and key is not None and hit[0] == key:
         return hit[1]
     cat = torch.cat([w.detach() for w in ws], 0).contiguous()
+    if key is None:
+        return cat
     # the entry holds the weights themselves: a replaced parameter cannot reuse their memory (and so
     # their key) while the entry lives
     object.__setattr__(module, cache_attr, (key, cat, tuple(ws)))
@@ -154,11 +156,13 @@ def _context_kv(module, ctx: torch.Tensor, heads: int):
     wkv = _cat_weight(module, ("to_k", "to_v"), "_wkv")
     # the parameters themselves (storage and version), not the concatenated copy, whose memory is
     # recycled when the weights change
-    pkey = tuple((p.data_ptr(), p._version, p.dtype) for m in (module.to_k, module.to_v)
-                 for p in (m.weight, m.bias) if p is not None)
-    key = (ctx.data_ptr(), tuple(ctx.shape), tuple(ctx.stride()), ctx.dtype, ctx._version, pkey, heads)
-    # a HIP graph records the projection itself; VP2P_CTX_CACHE=0 recomputes per call (A/B)
-    capturing = torch.cuda.is_current_stream_capturing() or not _CTX_CACHE
+    pkey = ops.version_key(*(p for m in (module.to_k, module.to_v) for p in (m.weight, m.bias) if p is not None))
+    ckey = ops.version_key(ctx)
+    key = (ckey, tuple(ctx.shape), tuple(ctx.stride()), pkey, heads)
+    # a HIP graph records the projection itself; VP2P_CTX_CACHE=0 recomputes per call (A/B); inference
+    # tensors have no version counter to key on
+    capturing = (torch.cuda.is_current_stream_capturing() or not _CTX_CACHE or ckey is None
+                 or pkey is None)
     hit = getattr(module, "_ctx_kv", None)
     if hit is not None and hit[0] == key and not capturing:
         return hit[2], hit[3], hit[4]
@@ -250,28 +254,25 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
     bias = None
     if module.to_q.bias is not None:
         bias = torch.cat([module.to_q.bias, module.to_k.bias, module.to_v.bias])
-    qkv = ops.linear(x, w, bias)
-    if autograd.needs_grad(qkv):
+    if autograd.needs_grad(x, w, bias):
         if not plain or temporal_layout != "bf":
             raise NotImplementedError("backward through a P2P-controlled or '(b d) f c' temporal attention")
         sh = frame_parallel.active()
         if sh is not None and sh.world > 1:
-            # frames sharded under autograd: the all-to-all frames <-> tokens and its adjoint
+            # frames sharded under autograd: the all-to-all frames <-> tokens (of the normed hidden
+            # state: C per token, the projection runs on the token slice) and its adjoint
             Bq = x.shape[0] // video_length
-            qkv = frame_parallel.to_tokens(sh, qkv, Bq)
+            qkv = ops.linear(frame_parallel.to_tokens(sh, x, Bq), w, bias)
             out = autograd.TemporalAttention.apply(qkv, video_length * sh.world, h, module.scale)
             return to_out(frame_parallel.to_frames(sh, out, Bq))
-        return to_out(autograd.TemporalAttention.apply(qkv, video_length, h, module.scale))
+        return to_out(autograd.TemporalAttention.apply(ops.linear(x, w, bias), video_length, h, module.scale))
     shard = frame_parallel.active() if temporal_layout == "bf" else None
-    if shard is not None:
-        # frames are sharded: regroup to all frames x this rank's token slice (one all-to-all)
-        B = x.shape[0] // video_length
-        qkv = shard.to_tokens(qkv, B)
-    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    if shard is not None and shard.world <= 1:
+        shard = None
     if temporal_layout == "bf":
         f = video_length * (shard.world if shard is not None else 1)
-        B = qkv.shape[0] // f
-        N = qkv.shape[1]
+        B = x.shape[0] // video_length
+        N = x.shape[1] // (shard.world if shard is not None else 1)   # this rank's token slice
     else:  # the reference's '(b d) f c' tensor
         f = x.shape[1]
         P0 = getattr(controller, "batch_size", 0) or 0
@@ -284,26 +285,50 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
     if call.store or not fused:
         probs = torch.empty(B * N * h, f, f, device=dev, dtype=torch.float32)
     replace = bool(call.self_replace) and P > 0
-    if temporal_layout == "bf":
-        out = ops.temporal_attention_p2p(q, k, v, f, h, prompts=P, self_replace=replace, probs_out=probs,
-                                         scale=module.scale, cond_only=cond_only)
-    else:
-        out = ops.temporal_attention_p2p_bd(q, k, v, B, h, prompts=P, self_replace=replace, probs_out=probs,
-                                            scale=module.scale, cond_only=cond_only)
-    if not fused:
-        attn = controller(probs, False, place)
-        out = _pv_temporal(module, attn, v, B, f, N, temporal_layout == "bf")
-    elif controller is not None:
-        controller.fused_end(False, place, call, probs)
+
+    def kernel(xt):
+        """q|k|v projection + K3 (+ the foreign controller) on (B*f, n, C) tokens -> (B*f, n, C)."""
+        qkv = ops.linear(xt, w, bias)
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        if temporal_layout == "bf":
+            o = ops.temporal_attention_p2p(q, k, v, f, h, prompts=P, self_replace=replace, probs_out=probs,
+                                           scale=module.scale, cond_only=cond_only)
+        else:
+            o = ops.temporal_attention_p2p_bd(q, k, v, B, h, prompts=P, self_replace=replace, probs_out=probs,
+                                              scale=module.scale, cond_only=cond_only)
+        if not fused:
+            attn = controller(probs, False, place)
+            o = _pv_temporal(module, attn, v, B, f, qkv.shape[1] if temporal_layout == "bf" else N, temporal_layout == "bf")
+        return o
+
     if shard is not None:
-        out = shard.to_frames(out, B)
+        # one exchange of the normed hidden state per direction, in token pieces that overlap the
+        # kernel (one piece when the probabilities are materialised for a controller)
+        out = shard.temporal_exchange(x, B, kernel, 1 if probs is not None else _temporal_chunks(x, shard.world))
+    else:
+        out = kernel(x)
+    if fused and controller is not None:
+        controller.fused_end(False, place, call, probs)
     return _out_proj(to_out, out, residual)
+
+
+def _temporal_chunks(x: torch.Tensor, world: int) -> int:
+    """Token pieces of the sharded attn_temp exchange: 4 when each piece still moves >= 1 MiB per
+    rank, else 1 (small messages are latency-bound; splitting them only adds launches)."""
+    per_rank = x.numel() * x.element_size() // max(world, 1)
+    return 4 if per_rank >= 4 << 20 and (x.shape[1] // world) % 4 == 0 else 1
+
+
+def _plain_linear(m) -> bool:
+    """A bare nn.Linear with no forward hooks: only then may its weights be used directly (a subclass
+    such as a LoRA-compatible Linear, or a hooked module, is called as a module)."""
+    return type(m) is nn.Linear and not (m._forward_hooks or m._forward_pre_hooks)
 
 
 def _linear_out(to_out, out):
     """``to_out(out)`` at inference through ``ops.linear`` (K10's GEMM core for the K = 320 projections
     of the 64x64 latents, hipBLASLt elsewhere); any other module, or autograd, calls it as is."""
-    if isinstance(to_out, nn.Linear) and not torch.is_grad_enabled():
+    if _plain_linear(to_out) and not torch.is_grad_enabled():
         return ops.linear(out, to_out.weight, to_out.bias)
     return to_out(out)
 
@@ -312,7 +337,7 @@ def _linear_out_add(to_out, out, residual):
     """residual + to_out(out) (the block's residual add, attention.py:247-262) at inference: the add
     in K10's epilogue where the projection runs on K10 (``ops.linear_add``), the two roundings of
     the reference (projection, then sum) either way."""
-    if isinstance(to_out, nn.Linear) and not torch.is_grad_enabled() and out.is_contiguous():
+    if _plain_linear(to_out) and not torch.is_grad_enabled() and out.is_contiguous():
         return ops.linear_add(out, to_out.weight, to_out.bias, residual)
     return to_out(out) + residual
 
@@ -324,7 +349,7 @@ def _out_proj(to_out, out, residual):
     hipBLASLt + a separate add (``ops.CONV.pick``, the same per-shape choice as the proj_out fusion)."""
     if residual is None:
         return to_out(out)
-    if torch.is_grad_enabled() or not isinstance(to_out, nn.Linear) or not out.is_contiguous() \
+    if torch.is_grad_enabled() or not _plain_linear(to_out) or not out.is_contiguous() \
             or residual.shape[:-1] != out.shape[:-1] or residual.dtype != out.dtype:
         return to_out(out) + residual
     res = residual.contiguous()

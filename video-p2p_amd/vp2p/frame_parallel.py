@@ -137,7 +137,11 @@ class FrameShard:
             return dist.broadcast(t, src=self.src0, group=self.group, async_op=True)
         n = flat.numel() // self.world
         mine = flat[self.rank * n:(self.rank + 1) * n]
-        w1 = dist.scatter(mine, list(flat.split(n)) if self.rank == 0 else None, src=self.src0, group=self.group,
+        # the root already holds its slice in place: its scatter output is a scratch buffer, so no
+        # scatter source aliases a destination (the all-gather below is NCCL's in-place form:
+        # sendbuff = recvbuff + rank * count)
+        out = torch.empty_like(mine) if self.rank == 0 else mine
+        w1 = dist.scatter(out, list(flat.split(n)) if self.rank == 0 else None, src=self.src0, group=self.group,
                           async_op=True)
         if self.staged:          # gloo runs async ops on worker threads, unordered: finish the scatter
             w1.wait()
@@ -175,6 +179,62 @@ class FrameShard:
         recv = torch.empty_like(send)                                              # (src slice, b, fl, Nl, C)
         self._all_to_all(recv, send)
         return recv.permute(1, 2, 0, 3, 4).reshape(batch * fl, G * Nl, C)
+
+    def _a2a_start(self, out: torch.Tensor, inp: torch.Tensor):
+        """Start an all-to-all of ``inp`` (dim 0 = destination rank) into ``out`` (dim 0 = source);
+        returns a handle.  RCCL: the exchange runs on the group's stream and ``wait()`` orders the
+        current stream after it; gloo (host-staged) completes it here."""
+        if self.staged and inp.is_cuda:
+            self._all_to_all(out, inp)
+            return _Done()
+        return dist.all_to_all_single(out, inp, group=self.group, async_op=True)
+
+    def temporal_exchange(self, x: torch.Tensor, batch: int, fn, chunks: int = 1) -> torch.Tensor:
+        """attn_temp over sharded frames (attention.py:262-268): ``fn`` maps (batch*f, n, C) -- every
+        frame of the clip for n tokens -- to (batch*f, n, Cout), independently per token (the qkv
+        projection, the temporal kernel and its P2P edit).  ``x`` is this rank's (batch*fl, N, C)
+        frames of the block's normed hidden state; returns this rank's (batch*fl, N, Cout) frames of
+        fn's result.
+
+        Only x (C per token) crosses the link, not the projected q|k|v (3C): the projection is per
+        token, so it runs after the exchange on the rank's token slice.  The slice is cut into
+        ``chunks`` token pieces, each an all-to-all of its own issued up front: piece k+1 moves while
+        fn runs on piece k, and piece k's output starts home before piece k+1's fn."""
+        G = self.world
+        Bfl, N, C = x.shape
+        fl = Bfl // batch
+        if N % G:
+            raise ValueError(f"{N} tokens do not split over {G} ranks")
+        Nl = N // G
+        if chunks < 1 or Nl % chunks:
+            chunks = 1
+        Nc = Nl // chunks
+        xs = x.reshape(batch, fl, G, Nl, C)
+        sends, recvs, works = [], [], []
+        for c in range(chunks):
+            # to destination j: token piece c of slice j of every local frame, laid out (j, b, fl, Nc, C)
+            s = xs[:, :, :, c * Nc:(c + 1) * Nc].permute(2, 0, 1, 3, 4).contiguous()
+            r = torch.empty_like(s)                                    # (src, b, fl, Nc, C)
+            works.append(self._a2a_start(r, s))
+            sends.append(s)
+            recvs.append(r)
+        out = None
+        backs = []
+        for c in range(chunks):
+            works[c].wait()
+            xt = recvs[c].permute(1, 0, 2, 3, 4).reshape(batch * G * fl, Nc, C)     # frames src*fl + i
+            y = fn(xt)
+            Co = y.shape[-1]
+            s = y.reshape(batch, G, fl, Nc, Co).permute(1, 0, 2, 3, 4).contiguous()  # (dst, b, fl, Nc, Co)
+            r = torch.empty_like(s)                                                 # (src, b, fl, Nc, Co)
+            backs.append((self._a2a_start(r, s), s, r))
+            if out is None:
+                out = torch.empty(batch, fl, G, Nl, Co, device=x.device, dtype=y.dtype)
+        for c, (wk, _, r) in enumerate(backs):
+            wk.wait()
+            out[:, :, :, c * Nc:(c + 1) * Nc] = r.permute(1, 2, 0, 3, 4)
+        del sends
+        return out.reshape(batch * fl, N, out.shape[-1])
 
     def local(self, x: torch.Tensor, dim: int = 2) -> torch.Tensor:
         """This rank's frames of a full-clip tensor (frame axis ``dim``)."""

@@ -36,6 +36,22 @@ def _dtype(*ts):
     return _DT[d]
 
 
+def version_key(*ts):
+    """Key of the current contents of ``ts`` for a derived-tensor cache: each tensor's storage and
+    version counter (None for an absent tensor).  None when one of them is an inference tensor
+    (``torch.inference_mode``): those have no version counter, so an in-place write could not be
+    detected -- the caller then recomputes and caches nothing."""
+    out = []
+    for t in ts:
+        if t is None:
+            out.append(None)
+        elif t.is_inference():
+            return None
+        else:
+            out.append((t.data_ptr(), t._version, t.dtype, t.device))
+    return tuple(out)
+
+
 def _stream():
     """The current HIP stream of the current device (the raw handle: no Stream object per launch)."""
     return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice()))

@@ -150,12 +150,20 @@ class VideoP2PPipeline:
 
 
     def _graphed(self, controller, prompts, lat0, emb0, steps, guidance, fast, uncond_pre, callback, callback_steps):
-        key = (id(controller), tuple(lat0.shape), tuple(emb0.shape), steps, float(guidance), bool(fast),
+        """ONE captured edit is kept: an edit with another controller or shape replaces it, and the
+        old graphs, their private memory pool and the old controller are released first (a session
+        that builds a controller per edit stays bounded)."""
+        key = (tuple(lat0.shape), tuple(emb0.shape), steps, float(guidance), bool(fast),
                uncond_pre is not None, str(lat0.device))
-        cache = self.__dict__.setdefault("_graph_cache", {})
-        ge = cache.get(key)
-        if ge is None or ge.controller is not controller:
-            ge = cache[key] = _GraphedEdit(self, controller, prompts, lat0, emb0, steps, guidance, fast, uncond_pre)
+        hit = self.__dict__.get("_graph_cache")
+        if hit is not None and hit[0] == key and hit[1].controller is controller:
+            ge = hit[1]
+        else:
+            self.__dict__["_graph_cache"] = None
+            del hit
+            torch.cuda.synchronize(lat0.device)
+            ge = _GraphedEdit(self, controller, prompts, lat0, emb0, steps, guidance, fast, uncond_pre)
+            self.__dict__["_graph_cache"] = (key, ge)
         return ge.run(lat0, emb0, uncond_pre, callback, callback_steps)
 
 
@@ -220,7 +228,8 @@ class _GraphedEdit:
         for i, (g, t) in enumerate(zip(self.graphs, self.ts)):
             g.replay()
             if callback is not None and i % callback_steps == 0:
-                callback(i, t, self.lats[i])
+                # a copy: the graph pool's buffer is rewritten by the next replay
+                callback(i, t, self.lats[i].clone())
         return self.lats[-1].clone()
 
 

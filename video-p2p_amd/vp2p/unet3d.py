@@ -147,9 +147,9 @@ class InflatedConv3d(nn.Conv2d):
         nothing to the sums."""
         cout, cin = self.weight.shape[:2]
         cin_p, cout_p = -(-cin // 64) * 64, -(-cout // 160) * 160
-        key = (self.weight.data_ptr(), self.weight._version, None if self.bias is None else self.bias._version)
+        key = ops.version_key(self.weight, self.bias)
         cached = self.__dict__.get("_k10_pad")
-        if cached is None or cached[0] != key:
+        if cached is None or key is None or cached[0] != key:
             wp = self.weight.new_zeros((cout_p, cin_p, 3, 3))
             wp[:cout, :cin] = self.weight.detach()
             wp = wp.contiguous(memory_format=torch.channels_last)
@@ -222,13 +222,14 @@ class GEGLU(nn.Module):
 
     def _interleaved(self):
         w, b = self.proj.weight, self.proj.bias
-        key = (w.data_ptr(), w._version, None if b is None else (b.data_ptr(), b._version))
+        key = ops.version_key(w, b)
         hit = getattr(self, "_il", None)
-        if hit is None or hit[0] != key:
+        if hit is None or key is None or hit[0] != key:
             with torch.no_grad():
                 # held with the entry: the parameters' memory cannot be recycled under the key
                 hit = (key, ops.geglu_interleave(w.detach(), None if b is None else b.detach()), (w, b))
-            object.__setattr__(self, "_il", hit)
+            if key is not None:
+                object.__setattr__(self, "_il", hit)
         return hit[1]
 
 
@@ -242,7 +243,10 @@ class FeedForward(nn.Module):
         """``residual``: residual + ff(x) (the block's add, attention.py:259), fused at inference."""
         x = self.net[1](self.net[0](x))
         out = self.net[2]
-        if not torch.is_grad_enabled():
+        # the fused path only for a plain Linear without hooks (a wrapped / LoRA / quantised output
+        # layer, or one with forward hooks, is called as a module)
+        plain = type(out) is nn.Linear and not (out._forward_hooks or out._forward_pre_hooks)
+        if plain and not torch.is_grad_enabled():
             if residual is not None:
                 return ops.linear_add(x, out.weight, out.bias, residual)
             return ops.linear(x, out.weight, out.bias)
@@ -524,7 +528,10 @@ class UNet3DConditionModel(nn.Module):
         K2 layout across the denoising steps (``attention._context_kv``)."""
         if torch.cuda.is_current_stream_capturing():      # a HIP graph re-reads its input at every replay
             return eh.to(self.dtype)
-        key = (eh.data_ptr(), tuple(eh.shape), tuple(eh.stride()), eh.dtype, eh.device, eh._version, self.dtype)
+        vk = ops.version_key(eh)
+        if vk is None:                      # inference tensor: no version counter, nothing to key on
+            return eh.to(self.dtype)
+        key = (vk, tuple(eh.shape), tuple(eh.stride()), self.dtype)
         hit = self.__dict__.get("_ctx_cache")
         if hit is not None and hit[0] == key:
             return hit[2]
@@ -543,13 +550,14 @@ class UNet3DConditionModel(nn.Module):
             rs = [m for m in self.modules() if isinstance(m, ResnetBlock3D)]
             object.__setattr__(self, "_resnets", rs)
         ps = [p for r in rs for p in (r.time_emb_proj.weight, r.time_emb_proj.bias)]
-        key = tuple((p.data_ptr(), p._version, p.dtype, p.device) for p in ps)
+        key = ops.version_key(*ps)
         hit = self.__dict__.get("_temb_cat")
-        if hit is None or hit[0] != key:
+        if hit is None or key is None or hit[0] != key:
             w = torch.cat([r.time_emb_proj.weight.detach() for r in rs]).contiguous()
             b = torch.cat([r.time_emb_proj.bias.detach() for r in rs])
             hit = (key, w, b, tuple(ps))      # the parameters held: their memory keeps its key
-            object.__setattr__(self, "_temb_cat", hit)
+            if key is not None:
+                object.__setattr__(self, "_temb_cat", hit)
         out = F.linear(F.silu(emb), hit[1], hit[2])
         off = 0
         for r in rs:
