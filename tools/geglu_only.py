@@ -1,5 +1,5 @@
 """Run only the fused K10 GEGLU projection N times (a rocprofv3 --pmc target).
-usage: python tools/geglu_only.py M K INNER [REPS]   (VP2P_CONV_TILE picks the tile)"""
+usage: python tools/geglu_only.py M K INNER [REPS]"""
 import os
 import sys
 

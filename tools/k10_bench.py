@@ -27,7 +27,7 @@ def timeit(fn, n=10):
     return sorted(ts)[2]
 
 
-lib = os.path.basename(os.environ.get("VP2P_LIB", "libvp2p_hip.so")) + ":" + os.environ.get("VP2P_CONV_TILE", "auto")
+lib = os.path.basename(os.environ.get("VP2P_LIB", "libvp2p_hip.so"))
 g = torch.Generator(device="cuda").manual_seed(0)
 rows = []
 # 3x3 convs: (n, cin, h, cout, stride, residual)

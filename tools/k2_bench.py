@@ -1,6 +1,6 @@
 """K2 (hooked cross-attention + fused P2P edit) timing at the edit's shapes, one JSON line per case.
 
-  python tools/k2_bench.py [--iters 50]        (VP2P_K2=v1 selects the previous kernel for an A/B)
+  python tools/k2_bench.py [--iters 50]
 
 Cases: the rabbit edit (AttentionRefine + Reweight) at B = 4 (2 prompts x CFG), 8 frames:
 res-64 (4096 tokens, C 320, d 40) edit on / off, res-16 with the LocalBlend sum (256 tokens, C 1280),
@@ -53,7 +53,7 @@ def main():
         e.synchronize()
         us = s.elapsed_time(e) / args.iters * 1e3
         nbytes = 2 * (2 * B * f * hw * C + 2 * B * 77 * C)
-        print(json.dumps({"case": name, "kernel": os.environ.get("VP2P_K2", "v2"), "us": round(us, 2),
+        print(json.dumps({"case": name, "us": round(us, 2),
                           "gbs": round(nbytes / us / 1e3, 1), "frac_8tbs": round(nbytes / us / 1e3 / 8000, 4),
                           "checksum": float(out.float().abs().sum()),
                           "lb_checksum": None if acc is None else float(acc.sum())}), flush=True)

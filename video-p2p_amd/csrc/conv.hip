@@ -108,7 +108,6 @@ template <int CF> struct GCfg;
 template <> struct GCfg<0> : GTile<128, 160, 4, 2> {};
 template <> struct GCfg<1> : GTile<256, 160, 4, 3> {};
 template <> struct GCfg<2> : GTile<256, 320, 8, 2> {};
-template <> struct GCfg<3> : GTile<256, 320, 8, 4, 32> {};
 constexpr int G_STAGE = GCfg<0>::STAGE;
 constexpr int G_LDS = GCfg<0>::LDS;
 
@@ -491,11 +490,6 @@ __global__ __launch_bounds__(512, 1) void conv_kernel_w(const vp2p_conv_args a) 
   conv_tile<KS, EPI, AM, 2>(a);
 }
 
-template <int KS, int EPI = 0, int AM = 1>
-__global__ __launch_bounds__(512, 1) void conv_kernel_d(const vp2p_conv_args a) {
-  conv_tile<KS, EPI, AM, 3>(a);
-}
-
 template <int KS, int EPI, int AM, int CF> struct ConvKernel;
 template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 0> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, AM>); }
@@ -505,9 +499,6 @@ template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 1> {
 };
 template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 2> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_w<KS, EPI, AM>); }
-};
-template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 3> {
-  static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_d<KS, EPI, AM>); }
 };
 
 // split-K second pass: y = round(round(sum_s ws[s] + bias) + residual), the one-pass roundings
@@ -551,10 +542,8 @@ static int launch_g1(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL((conv_kernel_g<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   else if constexpr (CF == 1)
     hipLaunchKernelGGL((conv_kernel_b<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
-  else if constexpr (CF == 2)
-    hipLaunchKernelGGL((conv_kernel_w<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   else
-    hipLaunchKernelGGL((conv_kernel_d<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
+    hipLaunchKernelGGL((conv_kernel_w<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
@@ -570,33 +559,18 @@ static int launch_g(const vp2p_conv_args& a, dim3 grid, int am, hipStream_t s) {
 // CF 1 (256 x 160, 3 stages): measured (profiles/r03_k10_tile_ab.jsonl, bit-equal) to win only on the
 // long-K 1x1 GEMMs (M 131072, K 1280, N 320: 185.5 -> 170.2 us), 2-8 % slower on the 3x3 convs and
 // the K = 320 GEMM / GEGLU shapes.  CF 2 (256 x 320 wide): Cout % 320 == 0 and enough
-// tiles to give every CU one.  VP2P_CONV_TILE=128 | 256 | wide | deep | auto (default) -- A/B, read once.
-static int tile_mode() {
-  static const int m = [] {
-    const char* e = getenv("VP2P_CONV_TILE");
-    if (e && e[0] == '1') return 0;
-    if (e && e[0] == '2') return 2;
-    if (e && e[0] == 'w') return 3;
-    if (e && e[0] == 'd') return 4;
-    return 1;
-  }();
-  return m;
-}
-
+// tiles to give every CU one.  (A wide tile on 32-channel K-steps in a four-stage ring, three steps'
+// DMA in flight, measured bit-equal but 4-10 % slower on every shape:
+// profiles/r03_k10_deep_rejected.jsonl.)
 // auto: the wide tile wherever it gives every CU a tile (measured, profiles/r03_k10_wide_ab.jsonl,
 // bit-equal: 3x3 convs at 64^2 / 32^2 -6..-13 %, 1x1 GEMMs M 131072 K 320 / 1280 N 320 -5 / -21 %,
 // M 32768 K 640 N 640 -10 %; slower where it leaves CUs idle: 128-tile grids +3..+50 %)
 static bool wide_auto(const vp2p_conv_args* a) { return a->kernel == 3 || a->kernel == 1; }
 
 static int pick_tile(const vp2p_conv_args* a, int64_t M) {
-  const int mode = tile_mode();
-  if (mode == 0) return 0;
   const int64_t tiles_b = (M + 255) / 256 * (a->cout / BN);
   const bool wide_ok = a->cout % 320 == 0;    // plain and GEGLU epilogues (GEGLU: profiles/r03_k10_geglu_wide_ab.jsonl)
   const int64_t tiles_w = (M + 255) / 256 * (a->cout / 320);
-  if (mode == 2) return 1;
-  if (mode == 3) return a->cout % 320 == 0 ? 2 : 0;   // GEGLU included (A/B)
-  if (mode == 4) return a->cout % 320 == 0 ? 3 : 0;
   if (wide_ok && tiles_w >= 256 && wide_auto(a)) return 2;
   return (tiles_b >= 256 && a->kernel == 1 && a->cin >= 1280) ? 1 : 0;
 }
@@ -686,10 +660,6 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
     const dim3 gw((unsigned)((M + 255) / 256 * (a->cout / 320)));
     if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 2>(*a, gw, fast, s);
     else rc = a->kernel == 3 ? conv::launch_g<3, 0, 2>(*a, gw, fast, s) : conv::launch_g<1, 0, 2>(*a, gw, fast, s);
-  } else if (cf == 3) {
-    const dim3 gw((unsigned)((M + 255) / 256 * (a->cout / 320)));
-    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 3>(*a, gw, fast, s);
-    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 3>(*a, gw, fast, s) : conv::launch_g<1, 0, 3>(*a, gw, fast, s);
   } else if (a->epilogue == VP2P_CONV_EPI_GEGLU) {
     rc = conv::launch_g<1, 1>(*a, grid, fast, s);
   } else {

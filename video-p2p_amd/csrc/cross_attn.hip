@@ -352,14 +352,14 @@ struct CrossV3Cfg {
 // T77: the SD text context (77 tokens, KB = 3): in the last 32-key block only keys 64..76 are real,
 // so accumulator registers 8..15 (keys 80..95 for both lane halves) are never computed through exp
 // and the block's second PV k-step (keys 80..95) is skipped.
-// MODE 0: Q fragments loaded straight from HBM one block ahead; 1: the same two blocks ahead;
+// MODE 0: Q fragments loaded straight from HBM one block ahead;
 // 2 ("staged", needs tokens_q % 32 == 0): a wave moves its block's Q rows and O rows as whole
 // 2d-byte row segments (5 / 10 / 20 lanes per row for d = 40 / 80 / 160) through a private LDS
 // tile, instead of fragment-shaped loads / stores that touch 32 rows x 16-32 B per instruction.
 template <int D, int KB, bool T77 = false, int MODE = 0>
 __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(const vp2p_cross_attn_args a, int iters, int b0,
                                                                                int nx, int rows) {
-  constexpr int PF = MODE == 1 ? 2 : 1;
+  static_assert(MODE == 0 || MODE == 2, "Q path");
   constexpr bool STG = MODE == 2;
   using T = bf16;
   using M = Mfma<T>;
@@ -460,18 +460,10 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
         Qs[row * QROW + D + (i - row * (C::DP - D))] = (T)0.f;
       }
   }
-  bf16x8 qn[C::KS], qn2[C::KS];
+  bf16x8 qn[C::KS];
   if constexpr (STG) load_raw(qi, fr, pos);
   else load_q(qi, fr, pos, qn);
   int fr_n = fr, pos_n = pos;          // (frame, token) of block qi
-  int qi2 = qi, fr2 = fr, pos2 = pos;  // PF 2: of the block fetched two ahead
-  if constexpr (PF == 2) {
-    if (iters > 1) {
-      advance(fr2, pos2);
-      qi2 += step;
-      load_q(qi2, fr2, pos2, qn2);
-    }
-  }
 
   for (int it = 0; it < iters; ++it) {
     bf16x8 qf[C::KS];
@@ -496,17 +488,6 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
       }
 #pragma unroll
       for (int s = 0; s < C::KS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qs + r * QROW + 16 * s + 8 * h);
-    } else if constexpr (PF == 2) {
-      if (it + 1 < iters) {
-#pragma unroll
-        for (int s = 0; s < C::KS; ++s) qn[s] = qn2[s];
-        qi = qi2, fr_n = fr2, pos_n = pos2;
-        if (it + 2 < iters) {
-          advance(fr2, pos2);
-          qi2 += step;
-          load_q(qi2, fr2, pos2, qn2);
-        }
-      }
     } else if (it + 1 < iters) {
       advance(fr_n, pos_n);
       qi += step;
@@ -905,54 +886,12 @@ static int cross_pad_dims(int head_dim, int dtype, int& dp, int& dv) {
 #undef VP2P_DIMS
 }
 
-// VP2P_K2=v1: A/B switch for the non-edit launches (default v3), read once
-static int cross_nonedit_kernel() {
-  static const int k = [] {
-    const char* e = getenv("VP2P_K2");
-    return (e && e[0] == 'v' && e[1] == '1') ? 1 : 3;
-  }();
-  return k;
-}
-
-// VP2P_K2_EDIT=v1: A/B switch of the edited half back to v1 (default v3e), read once
-static int cross_edit_kernel() {
-  static const int k = [] {
-    const char* e = getenv("VP2P_K2_EDIT");
-    return (e && e[0] == 'v' && e[1] == '1') ? 1 : 3;
-  }();
-  return k;
-}
-
-// VP2P_K2_WGCU=n: v3 grid target of n workgroups per CU (default 4) -- an A/B switch, read once
-// (measured no faster at 6, 8, 12; nor two Q blocks ahead: profiles/r03_k2_v3_pf_wgcu_ab.jsonl)
-static int cross_v3_wgcu() {
-  static const int n = [] {
-    const char* e = getenv("VP2P_K2_WGCU");
-    const int v = e ? atoi(e) : 4;
-    return v >= 1 && v <= 64 ? v : 4;
-  }();
-  return n;
-}
 // v3's Q/O path (cross_attn_kernel_v3 MODE): staged rows (2) for d <= 80 -- res-64 non-edit launch
 // 53.8 -> 48.5 us, res-32 edit launch 56.5 -> 53.4 us, bit-equal (profiles/r03_k2_v3_staged_ab.jsonl)
 // -- and fragment loads (0) for d = 160, where the 20-lane rows cost occupancy (31.0 -> 36.4 us).
-// VP2P_K2_V3=0|1|2 forces a mode (A/B), read once.
-static int cross_v3_mode(int d) {
-  static const int n = [] {
-    const char* e = getenv("VP2P_K2_V3");
-    return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
-  }();
-  return n >= 0 ? n : (d <= 80 ? 2 : 0);
-}
-
-// VP2P_K2_GRID=3d: A/B switch back to v3's (x, row, head) grid (default: 1-D, XCD-grouped), read once
-static bool cross_grid_1d() {
-  static const bool g = [] {
-    const char* e = getenv("VP2P_K2_GRID");
-    return !(e && e[0] == '3');
-  }();
-  return g;
-}
+// The grid targets 4 workgroups per CU over (row, head), 1-D and XCD-grouped (measured no faster at
+// 6, 8, 12 per CU, nor with two Q blocks ahead: profiles/r03_k2_v3_pf_wgcu_ab.jsonl).
+constexpr int kCrossV3WgPerCu = 4;
 
 template <typename T, int D, int KB>
 static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
@@ -964,39 +903,35 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
     const int64_t qblocks = (FQ + 31) / 32;
     const int64_t per_wg = (qblocks + 3) / 4;                   // iterations of one stream, all blocks
     const int64_t gh = (int64_t)rows * a->heads;
-    // ~cross_v3_wgcu() workgroups per CU over the (row, head) grid; each stream then loops `iters` blocks
-    const int64_t target = 256 * cross_v3_wgcu();
+    // ~kCrossV3WgPerCu workgroups per CU over the (row, head) grid; each stream then loops `iters` blocks
+    const int64_t target = 256 * kCrossV3WgPerCu;
     int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (target + gh - 1) / gh));
     const int iters = (int)((per_wg + nx - 1) / nx);
     nx = (per_wg + iters - 1) / iters;
     if (rows > 65535 || a->heads > 65535 || nx > 0x7fffffff) return VP2P_E_SHAPE;
     const int sets = a->lb_sets == 2 ? 2 : 1;
     const bool t77 = KB == 3 && a->tokens_kv == 77;
-    int mode = cross_v3_mode(D);
-    if (mode == 2 && a->tokens_q % 32) mode = 0;             // staged rows need whole blocks per frame
+    // staged rows need whole blocks per frame
+    const int mode = (D <= 80 && a->tokens_q % 32 == 0) ? 2 : 0;
     size_t lds = (size_t)V3::LDS + (size_t)sets * a->tokens_kv * sizeof(float);
     if (mode == 2) lds = ((lds + 15) & ~(size_t)15) + (size_t)4 * 32 * (CrossCfg<bf16, D>::DP + 8) * 2;
     const void* fn = nullptr;
-    switch (mode * 2 + (t77 ? 1 : 0)) {
+    switch (mode + (t77 ? 1 : 0)) {
       case 0: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, false, 0>); break;
       case 1: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true, 0>); break;
-      case 2: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, false, 1>); break;
-      case 3: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true, 1>); break;
-      case 4: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, false, 2>); break;
+      case 2: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, false, 2>); break;
       default: fn = reinterpret_cast<const void*>(&cross_attn_kernel_v3<D, KB, true, 2>); break;
     }
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
         lds > 160 * 1024)
       return VP2P_E_LAUNCH;
-    const bool g1 = cross_grid_1d() && nx * rows * a->heads <= 0x7fffffff;
+    const bool g1 = nx * rows * a->heads <= 0x7fffffff;
     const dim3 grid = g1 ? dim3((unsigned)(nx * rows * a->heads)) : dim3((unsigned)nx, (unsigned)rows, (unsigned)a->heads);
     const int nx1 = g1 ? (int)nx : 0;
-    switch (mode * 2 + (t77 ? 1 : 0)) {
+    switch (mode + (t77 ? 1 : 0)) {
       case 0: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, false, 0>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
       case 1: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true, 0>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
-      case 2: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, false, 1>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
-      case 3: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true, 1>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
-      case 4: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, false, 2>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
+      case 2: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, false, 2>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
       default: hipLaunchKernelGGL((cross_attn_kernel_v3<D, KB, true, 2>), grid, dim3(256), lds, s, *a, iters, b0, nx1, rows); break;
     }
     return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
@@ -1033,12 +968,12 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     const bool p2p = a->prompts > 0 && a->batch == (a->cond_only ? 1 : 2) * a->prompts;
     const bool edit = p2p && (a->edit_mode != VP2P_EDIT_NONE || a->reweight);
-    if (edit && !a->cond_only && cross_nonedit_kernel() == 3) {
+    if (edit && !a->cond_only) {
       const int rc = launch_v3(0, a->prompts);     // the unconditional half: plain attention on v3
       if (rc != VP2P_OK) return rc;
       g_first = 1;
     }
-    if (edit && a->prompts == 2 && cross_edit_kernel() == 3) {
+    if (edit && a->prompts == 2) {
       const int rc = launch_v3e();
       if (rc == VP2P_OK) {
         if (a->lb_acc) {
@@ -1053,7 +988,7 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
       }
       if (rc != VP2P_E_SHAPE) return rc;
     }
-    if (!edit && cross_nonedit_kernel() == 3) {
+    if (!edit) {
       const int rc = launch_v3(0, a->batch);
       if (rc != VP2P_OK) return rc;
       const int sets = a->lb_sets == 2 ? 2 : 1;

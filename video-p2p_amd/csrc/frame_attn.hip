@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void frame_attn_kernel
 constexpr int x2f_bufs(int D, int KT, bool FOLD) { return FOLD && D <= 64 && KT <= 128 ? 2 : 1; }
 
 template <int D, int KT, bool FOLD>
-__global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame_attn_args a, int head_fastest) {
+__global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame_attn_args a) {
   constexpr int kK1Bufs = x2f_bufs(D, KT, FOLD);
   using T = bf16;
   using M = Mfma<T>;
@@ -286,22 +286,11 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   const int FQ = a.frames * a.tokens_q;
   const int qblocks = (FQ + 255) >> 8;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  int b, head, qb;
-  if (head_fastest) {
-    // the a.heads workgroups of one query block are consecutive on one XCD: together their 80-B head
-    // slices cover whole 128-B lines of Q and O, read into and written back from one L2 at once
-    // (query-block-major order: each line is touched by ~2 heads' workgroups at different times)
-    const int per_b = qblocks * a.heads;
-    b = bid / per_b;
-    const int rem = bid - b * per_b;
-    qb = rem / a.heads;
-    head = rem - qb * a.heads;
-  } else {
-    const int bh = bid / qblocks;
-    qb = bid - bh * qblocks;
-    b = bh / a.heads;
-    head = bh - b * a.heads;
-  }
+  // (b, head)-major: all query blocks of one (b, head) on one XCD, its frame-0 K/V fetched into one L2
+  // (FETCH x2 + WRITE 427 MB at the res-64 launch vs 778 MB head-fastest, same time:
+  // profiles/r03_k1_grid_ab.txt)
+  const int bh = bid / qblocks, qb = bid - bh * qblocks;
+  const int b = bh / a.heads, head = bh - b * a.heads;
   const int Nk = a.tokens_kv;
   const float cs = a.q_prescaled ? 1.f : a.scale * kLog2e;
 
@@ -559,34 +548,13 @@ __global__ __launch_bounds__(256, 2) void frame_attn_kernel_x2f(const vp2p_frame
   }
 }
 
-// VP2P_K1_GRID=hf: A/B switch to the head-fastest grid, read once.  The default (b, head)-major grid
-// keeps all query blocks of one (b, head) on one XCD (its frame-0 K/V fetched into one L2): at the
-// res-64 launch FETCH x2 + WRITE = 427 MB vs 778 MB head-fastest (8 heads' K/V, 5.2 MB, thrash the
-// 4 MB L2), same time (0.868 vs 0.872 ms; profiles/r03_k1_grid_ab.txt)
-static int k1_head_fastest() {
-  static const int hf = [] {
-    const char* e = getenv("VP2P_K1_GRID");
-    return (e && e[0] == 'h') ? 1 : 0;
-  }();
-  return hf;
-}
-
-static bool x2f_d80_off() {   // VP2P_K1_D80=1set: A/B switch for the res-32 layers, read once
-  static const bool off = [] {
-    const char* e = getenv("VP2P_K1_D80");
-    return e && e[0] == '1';
-  }();
-  return off;
-}
-
 template <int D, int KT, bool FOLD>
 static int launch_x2f(const vp2p_frame_attn_args* a, int64_t nwg, hipStream_t stream) {
   constexpr int lds = x2f_bufs(D, KT, FOLD) * KT * (FrameCfg<bf16, D>::KROW + FrameCfg<bf16, D>::VROW) * 2;
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_x2f<D, KT, FOLD>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  hipLaunchKernelGGL((frame_attn_kernel_x2f<D, KT, FOLD>), dim3((unsigned)nwg), dim3(256), lds, stream, *a,
-                     k1_head_fastest());
+  hipLaunchKernelGGL((frame_attn_kernel_x2f<D, KT, FOLD>), dim3((unsigned)nwg), dim3(256), lds, stream, *a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
@@ -595,7 +563,6 @@ static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
   using C = FrameCfg<T, D>;
   const int FQ = a->frames * a->tokens_q;
   if constexpr (C::BF && C::ONES && D <= 80) {
-    if (D > 64 && x2f_d80_off()) goto one_set;
     constexpr int KT = D <= 64 ? 256 : 64;
     const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
     if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
@@ -607,7 +574,6 @@ static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
       if (a->q_prescaled) return launch_x2f<D, 128, true>(a, nwg, stream);
     return launch_x2f<D, KT, false>(a, nwg, stream);
   }
-one_set:
   const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 127) / 128);
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
   hipLaunchKernelGGL((frame_attn_kernel<T, D>), dim3((unsigned)nwg), dim3(256), C::LDS_BYTES, stream, *a);

@@ -30,7 +30,10 @@
 #include "frame_attn.hpp"
 
 #ifndef VP2P_K1_PP_SETS
-#define VP2P_K1_PP_SETS 4
+#define VP2P_K1_PP_SETS 3
+#endif
+#ifndef VP2P_K1_PP_WAVES
+#define VP2P_K1_PP_WAVES 4
 #endif
 
 namespace vp2p {
@@ -55,51 +58,46 @@ __device__ __forceinline__ bf16x8 ld128(const lchar* p) { return *reinterpret_ca
 __device__ __forceinline__ bf16x4 ldtr(const lchar* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(p));
 }
-// The inner loop is written out instruction by instruction: every MFMA, v_exp and v_cvt of it is a
-// volatile asm statement, so neither the IR passes nor the machine scheduler can move one (hipcc
-// otherwise clusters the exps in bursts of 8-40 between MFMAs).  Only the LDS reads, their waits
-// and the address arithmetic are left to the compiler.  Hazards the compiler cannot see are excluded
-// by the slot order (kernel header):
-//  * v_exp (trans) -> v_cvt reading it: an MFMA sits between them (a slot is cvts, exps, MFMA);
+// The inner loop is written out slot by slot: the MFMAs, v_exp and v_cvt of a slot are pinned to it
+// by sched_barrier(0), and the scores are made opaque at every block start (an empty asm) so no IR
+// pass hoists a block's exps into the previous one.  Only the LDS reads, their waits and the address
+// arithmetic are placed by the compiler.  The one inline-asm MFMA (PV into AGPRs, one wave per SIMD)
+// has hazards hipcc cannot see; the slot order excludes them:
 //  * v_cvt -> PV MFMA reading the packed P: one whole block apart;
-//  * QK^T MFMA -> v_exp reading the scores: >= 9 MFMA slots apart;
-//  * VALU write of P / O / Q' in the rare rescale -> MFMA: the s_nop 1 opening every block;
+//  * VALU write of P / O in the rare rescale -> MFMA: the s_nop 1 opening every block;
 //  * PV MFMA -> VALU read of O: o_fence() (two s_nop 7).
-__device__ __forceinline__ float vexp(float x) {
-  float y;
-  asm volatile("v_exp_f32 %0, %1" : "=v"(y) : "v"(x));
-  return y;
-}
 __device__ __forceinline__ uint32_t vcvt(float x, float y) {
-  uint32_t r;
-  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
-  return r;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x, y}, bf16x2));
 }
-// S^T = K . Q'^T, three k-steps; the chain's first step starts from 0
+// S^T = K . Q'^T, three k-steps (builtins: hipcc pads their hazards, including those of any copy it
+// makes of their operands)
 __device__ __forceinline__ void qk_first(f32x16& acc, const bf16x8& k, const bf16x8& q) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(k), "v"(q));
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k, q, f32x16{}, 0, 0, 0);
 }
 __device__ __forceinline__ void qk_next(f32x16& acc, const bf16x8& k, const bf16x8& q) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(k), "v"(q));
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k, q, acc, 0, 0, 0);
 }
 __device__ __forceinline__ void sb() { __builtin_amdgcn_sched_barrier(0); }
 
-// O^T += V^T . P^T into an accumulator-file tile (O stays in AGPRs).
+// O^T += V^T . P^T.  With one wave per SIMD O lives in the accumulator file (AGPRs) -- the arch
+// VGPRs hold everything else -- which takes inline asm (hipcc picks the register file of a builtin's
+// accumulator itself); with two waves per SIMD (256 registers per wave) everything, O included, fits
+// the arch VGPRs and the builtin is used, so hipcc pads every hazard.
+template <bool AGPR>
 __device__ __forceinline__ void pv(f32x16& o, const bf16x8& v, const u32x4& p) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(__builtin_bit_cast(bf16x8, p)));
-}
-
-// the slot-6 PV with the block's last bf16 packing behind it in the same statement
-__device__ __forceinline__ void pv_cvt(f32x16& o, const bf16x8& v, const u32x4& p, uint32_t& pk, float x, float y) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %3, %0\n\tv_cvt_pk_bf16_f32 %1, %4, %5"
-               : "+a"(o), "=&v"(pk) : "v"(v), "v"(__builtin_bit_cast(bf16x8, p)), "v"(x), "v"(y));
+  if constexpr (AGPR)
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o) : "v"(v), "v"(__builtin_bit_cast(bf16x8, p)));
+  else
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v, __builtin_bit_cast(bf16x8, p), o, 0, 0, 0);
 }
 
 }  // namespace
 
-template <int SETS>
-__global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_attn_args a) {
+template <int SETS, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(const vp2p_frame_attn_args a) {
   static_assert(SETS >= 2, "the QK^T of the last set rides in group 0 of the next block");
+  static_assert(WAVES == 4 || WAVES == 8, "one or two waves per SIMD");
+  constexpr bool OA = WAVES == 4;                   // O in the accumulator file
   using T = bf16;
   using M = Mfma<T>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -107,7 +105,7 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
 
   const int tid = threadIdx.x, l = tid & 63, r = l & 31, h = l >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int QW = 32 * SETS, QB = 4 * QW;
+  constexpr int QW = 32 * SETS, QB = WAVES * QW;
   const int FQ = a.frames * a.tokens_q;
   const int qblocks = (FQ + QB - 1) / QB;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -134,7 +132,7 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
     for (int s = 0; s < 3; ++s) qf[st][s] = qv ? M::row_frag(qrow, s, h, kD) : M::zero();
   }
 
-  // K / V tile DMA: wave w issues instructions n = w, w + 4, w + 8 (< 10) of each tile; lane l of
+  // K / V tile DMA: wave w issues instructions n = w, w + WAVES, ... (< 10) of each tile; lane l of
   // instruction n moves chunk 64n + l = (row, chunk-in-row) of the dense image
   const T* kb_ = static_cast<const T*>(a.k) + b * a.k_sb + head * kD;
   const T* vb_ = static_cast<const T*>(a.v) + b * a.v_sb + head * kD;
@@ -142,11 +140,11 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
       const_cast<T*>(kb_), 0, (uint32_t)((int64_t)(Nk - 1) * a.k_sn * 2 + kRowB), 0x00020000);
   const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<T*>(vb_), 0, (uint32_t)((int64_t)(Nk - 1) * a.v_sn * 2 + kRowB), 0x00020000);
-  constexpr int NDMA = (kDmaPerTile + 3) / 4;
+  constexpr int NDMA = (kDmaPerTile + WAVES - 1) / WAVES;
   uint32_t kvo[NDMA], vvo[NDMA];
 #pragma unroll
   for (int i = 0; i < NDMA; ++i) {
-    const int c = 64 * (w + 4 * i) + l, row = c / 5, ch = c - row * 5;
+    const int c = 64 * (w + WAVES * i) + l, row = c / 5, ch = c - row * 5;
     kvo[i] = (uint32_t)(row * a.k_sn * 2 + ch * 16);
     vvo[i] = (uint32_t)(row * a.v_sn * 2 + ch * 16);
   }
@@ -161,7 +159,7 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
     const uint32_t ks = (uint32_t)tt * k_tile_b, vs = (uint32_t)tt * v_tile_b;
 #pragma unroll
     for (int i = 0; i < NDMA; ++i) {
-      const int n = w + 4 * i;
+      const int n = w + WAVES * i;
       if (i + 1 < NDMA || n < kDmaPerTile) {
         const uint32_t kd = __builtin_amdgcn_readfirstlane(lds_base + kKRing + slot * kSlotB + n * 1024);
         const uint32_t vd = __builtin_amdgcn_readfirstlane(lds_base + kVRing + slot * kSlotB + n * 1024);
@@ -247,6 +245,8 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
   auto block = [&](const lchar* kb, const lchar* k2b, int krow, const lchar* vb, const lchar* v1b, int vrow) {
     sb();
     asm volatile("s_nop 1");
+#pragma unroll
+    for (int st = 0; st < SETS; ++st) asm volatile("" : "+v"(S[st]));
     auto v_tr = [&](int sp, int t) {
       const int rb = (vrow + 16 * sp) * kRowB + (t ? 64 : 0);
       const lchar* p = t ? v1b : vb;
@@ -264,47 +264,47 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
       uint32_t pn[8];
       f32x16 acc;
       const f32x16& sg = S[g];
-      // slot 0: exps 0-2 | PV(sp 0, tile 1)
-      e[0] = vexp(sg[0]); e[1] = vexp(sg[1]); e[2] = vexp(sg[2]);
-      pv(o[g][1], vf[0][1], P[g][0]);
-      if (last) vf[0][1] = v_tr(0, 1);
-      sb();
-      // slot 1: cvt 0-1, exps 3-4 | QK k-step 0
-      pn[0] = vcvt(e[0], e[1]);
-      e[3] = vexp(sg[3]); e[4] = vexp(sg[4]);
+      // slot 0: exps 0-2 | QK k-step 0
+      e[0] = fast_exp2(sg[0]); e[1] = fast_exp2(sg[1]); e[2] = fast_exp2(sg[2]);
       qk_first(acc, kf[0], qf[qs][0]);
       if (g == 0) kf[0] = ld128(kb + krow * kRowB);
       sb();
-      // slot 2: cvt 2-3, exps 5-6 | PV(sp 0, tile 0)
-      pn[1] = vcvt(e[2], e[3]);
-      e[5] = vexp(sg[5]); e[6] = vexp(sg[6]);
-      pv(o[g][0], vf[0][0], P[g][0]);
-      if (last) vf[0][0] = v_tr(0, 0);
+      // slot 1: cvt 0-1, exps 3-4 | PV(sp 0, tile 1)
+      pn[0] = vcvt(e[0], e[1]);
+      e[3] = fast_exp2(sg[3]); e[4] = fast_exp2(sg[4]);
+      pv<OA>(o[g][1], vf[0][1], P[g][0]);
+      if (last) vf[0][1] = v_tr(0, 1);
       sb();
-      // slot 3: cvt 4-5, exps 7-8 | QK k-step 1
-      pn[2] = vcvt(e[4], e[5]);
-      e[7] = vexp(sg[7]); e[8] = vexp(sg[8]);
+      // slot 2: cvt 2-3, exps 5-6 | QK k-step 1
+      pn[1] = vcvt(e[2], e[3]);
+      e[5] = fast_exp2(sg[5]); e[6] = fast_exp2(sg[6]);
       qk_next(acc, kf[1], qf[qs][1]);
       if (g == 0) kf[1] = ld128(kb + krow * kRowB + 32);
       sb();
-      // slot 4: cvt 6-7, exps 9-10 | PV(sp 1, tile 1)
-      pn[3] = vcvt(e[6], e[7]);
-      e[9] = vexp(sg[9]); e[10] = vexp(sg[10]);
-      pv(o[g][1], vf[1][1], P[g][1]);
-      if (last) vf[1][1] = v_tr(1, 1);
+      // slot 3: cvt 4-5, exps 7-8 | PV(sp 0, tile 0)
+      pn[2] = vcvt(e[4], e[5]);
+      e[7] = fast_exp2(sg[7]); e[8] = fast_exp2(sg[8]);
+      pv<OA>(o[g][0], vf[0][0], P[g][0]);
+      if (last) vf[0][0] = v_tr(0, 0);
       sb();
-      // slot 5: cvt 8-9, exps 11-13 | QK k-step 2 -> S[qs]
-      pn[4] = vcvt(e[8], e[9]);
-      e[11] = vexp(sg[11]); e[12] = vexp(sg[12]); e[13] = vexp(sg[13]);
+      // slot 4: cvt 6-7, exps 9-10 | QK k-step 2 -> S[qs]
+      pn[3] = vcvt(e[6], e[7]);
+      e[9] = fast_exp2(sg[9]); e[10] = fast_exp2(sg[10]);
       qk_next(acc, kf[2], qf[qs][2]);
       if (g == 0) kf[2] = ld128(k2b + krow * kRowB + 64);
       sb();
-      // slot 6: cvt 10-13, exps 14-15 | PV(sp 1, tile 0), cvt 14-15 (same statement: the MFMA
-      // separates the trans write of e15 from its read)
+      // slot 5: cvt 8-9, exps 11-13 | PV(sp 1, tile 1)
+      pn[4] = vcvt(e[8], e[9]);
+      e[11] = fast_exp2(sg[11]); e[12] = fast_exp2(sg[12]); e[13] = fast_exp2(sg[13]);
+      pv<OA>(o[g][1], vf[1][1], P[g][1]);
+      if (last) vf[1][1] = v_tr(1, 1);
+      sb();
+      // slot 6: cvt 10-13, exps 14-15 | PV(sp 1, tile 0) | cvt 14-15
       pn[5] = vcvt(e[10], e[11]);
       pn[6] = vcvt(e[12], e[13]);
-      e[14] = vexp(sg[14]); e[15] = vexp(sg[15]);
-      pv_cvt(o[g][0], vf[1][0], P[g][1], pn[7], e[14], e[15]);
+      e[14] = fast_exp2(sg[14]); e[15] = fast_exp2(sg[15]);
+      pv<OA>(o[g][0], vf[1][0], P[g][1]);
+      pn[7] = vcvt(e[14], e[15]);
       if (last) vf[1][0] = v_tr(1, 0);
       S[qs] = acc;
       P[g][0] = u32x4{pn[0], pn[1], pn[2], pn[3]};
@@ -315,7 +315,8 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
   // O reads by the VALU: past the last PV MFMA's write (>= 12 wait states for this 8-pass MFMA)
   auto o_fence = [&]() {
 #pragma unroll
-    for (int st = 0; st < SETS; ++st) asm volatile("s_nop 7\n\ts_nop 7" : "+a"(o[st][0]), "+a"(o[st][1]));
+    for (int st = 0; st < SETS; ++st)
+      if constexpr (OA) asm volatile("s_nop 7\n\ts_nop 7" : "+a"(o[st][0]), "+a"(o[st][1]));
   };
 
   for (int t = 0; t < ntiles; ++t) {
@@ -385,10 +386,10 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
   asm volatile("s_nop 1");
 #pragma unroll
   for (int st = 0; st < SETS; ++st) {
-    pv(o[st][1], vf[0][1], P[st][0]);
-    pv(o[st][0], vf[0][0], P[st][0]);
-    pv(o[st][1], vf[1][1], P[st][1]);
-    pv(o[st][0], vf[1][0], P[st][1]);
+    pv<OA>(o[st][1], vf[0][1], P[st][0]);
+    pv<OA>(o[st][0], vf[0][0], P[st][0]);
+    pv<OA>(o[st][1], vf[1][1], P[st][1]);
+    pv<OA>(o[st][0], vf[1][0], P[st][1]);
   }
   o_fence();
 
@@ -426,18 +427,18 @@ __global__ __launch_bounds__(256, 1) void frame_attn_kernel_pp(const vp2p_frame_
 }
 
 int launch_frame_attn_pp(const vp2p_frame_attn_args* a, hipStream_t stream) {
-  constexpr int SETS = VP2P_K1_PP_SETS;
+  constexpr int SETS = VP2P_K1_PP_SETS, WAVES = VP2P_K1_PP_WAVES;
   if (a->dtype != VP2P_BF16 || a->head_dim != kD || !a->q_prescaled || a->tokens_kv % kKT) return VP2P_E_SHAPE;
   // 32-bit buffer offsets: every key row of one (b, head) within 4 GiB
   if ((int64_t)a->tokens_kv * a->k_sn * 2 >= (1ll << 32) || (int64_t)a->tokens_kv * a->v_sn * 2 >= (1ll << 32))
     return VP2P_E_SHAPE;
   const int FQ = a->frames * a->tokens_q;
-  const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 128 * SETS - 1) / (128 * SETS));
+  const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 32 * SETS * WAVES - 1) / (32 * SETS * WAVES));
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_pp<SETS>),
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_pp<SETS, WAVES>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  hipLaunchKernelGGL((frame_attn_kernel_pp<SETS>), dim3((unsigned)nwg), dim3(256), kLdsBytes, stream, *a);
+  hipLaunchKernelGGL((frame_attn_kernel_pp<SETS, WAVES>), dim3((unsigned)nwg), dim3(64 * WAVES), kLdsBytes, stream, *a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 

@@ -40,10 +40,9 @@ struct TempCfg {
 // over blockIdx.y.  For d <= 80 the next prompt's Q, K and V rows are fetched while the current
 // prompt computes (and the first prompt's V with its Q and K), so each wave exposes one HBM
 // latency instead of two per prompt.
-// WPB waves per workgroup = WPB heads of the same token block.  WPB = 8 (every head of the SD
-// layers): a workgroup reads whole 2C-byte q / k / v rows and writes whole O rows, so no 128-byte line
-// is split between workgroups that run at different times (WPB = 4 splits each row's lines between
-// two), at the same 8 waves per CU.
+// WPB waves per workgroup = WPB heads of the same token block.  (Eight heads per workgroup -- whole
+// q / k / v / O rows per workgroup -- measured bit-equal but 6 % slower at res-64 and 45-52 % slower
+// at res-16: profiles/r03_k3_wpb8_rejected.jsonl.)
 template <typename T, int D, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB, sizeof(T) == 2 ? 8 / WPB : 1) void temporal_attn_p2p_kernel(const vp2p_temporal_attn_args a, int lf) {
   using M = Mfma<T>;
@@ -385,15 +384,6 @@ static int launch_temporal_long(const vp2p_temporal_attn_args* a, hipStream_t s)
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
-// VP2P_K3_WPB=8: eight heads per workgroup (A/B; default four), read once
-static int k3_wpb() {
-  static const int w = [] {
-    const char* e = getenv("VP2P_K3_WPB");
-    return (e && e[0] == '8') ? 8 : 4;
-  }();
-  return w;
-}
-
 template <typename T, int D>
 static int launch_temporal(const vp2p_temporal_attn_args* a, hipStream_t s) {
   if (a->frames > 64) return launch_temporal_long<T, D, 4>(a, s);
@@ -406,12 +396,8 @@ static int launch_temporal(const vp2p_temporal_attn_args* a, hipStream_t s) {
   const int groups = p2p ? (a->cond_only ? 1 : 2) : a->batch;
   const int64_t nwg = (int64_t)groups * ((a->tokens + G - 1) / G);
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-  if (a->heads % 8 == 0 && k3_wpb() == 8)
-    hipLaunchKernelGGL((temporal_attn_p2p_kernel<T, D, 8>), dim3((unsigned)nwg, (unsigned)(a->heads / 8)), dim3(512),
-                       8 * C::WAVE_LDS, s, *a, lf);
-  else
-    hipLaunchKernelGGL((temporal_attn_p2p_kernel<T, D, 4>), dim3((unsigned)nwg, (unsigned)((a->heads + 3) / 4)), dim3(256),
-                       4 * C::WAVE_LDS, s, *a, lf);
+  hipLaunchKernelGGL((temporal_attn_p2p_kernel<T, D, 4>), dim3((unsigned)nwg, (unsigned)((a->heads + 3) / 4)), dim3(256),
+                     4 * C::WAVE_LDS, s, *a, lf);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 

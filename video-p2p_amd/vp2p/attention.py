@@ -18,7 +18,6 @@ against the concatenated weights -- all bit-identical to the reference's per-row
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -142,7 +141,6 @@ class FrameAttention(CrossAttention):
         return self.to_out[1](_linear_out(self.to_out[0], out))
 
 
-_CTX_CACHE = os.environ.get("VP2P_CTX_CACHE", "1") != "0"
 
 
 def _context_kv(module, ctx: torch.Tensor, heads: int):
@@ -159,10 +157,8 @@ def _context_kv(module, ctx: torch.Tensor, heads: int):
     pkey = ops.version_key(*(p for m in (module.to_k, module.to_v) for p in (m.weight, m.bias) if p is not None))
     ckey = ops.version_key(ctx)
     key = (ckey, tuple(ctx.shape), tuple(ctx.stride()), pkey, heads)
-    # a HIP graph records the projection itself; VP2P_CTX_CACHE=0 recomputes per call (A/B); inference
-    # tensors have no version counter to key on
-    capturing = (torch.cuda.is_current_stream_capturing() or not _CTX_CACHE or ckey is None
-                 or pkey is None)
+    # a HIP graph records the projection itself; inference tensors have no version counter to key on
+    capturing = torch.cuda.is_current_stream_capturing() or ckey is None or pkey is None
     hit = getattr(module, "_ctx_kv", None)
     if hit is not None and hit[0] == key and not capturing:
         return hit[2], hit[3], hit[4]

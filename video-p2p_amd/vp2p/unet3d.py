@@ -18,7 +18,6 @@ There is no CPU or PyTorch-op path: the model runs on the GPU only.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -66,14 +65,11 @@ def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
     return ops.layer_norm(x, norm.weight, norm.bias, norm.eps)
 
 
-_FUSE_ADD_LN = os.environ.get("VP2P_FUSE_ADD_LN", "1") != "0"     # A/B switches for experiments
-_FUSE_GEGLU = os.environ.get("VP2P_FUSE_GEGLU", "1") != "0"
-_FUSE_OUT_RES = os.environ.get("VP2P_FUSE_OUT_RES", "0") == "1"   # measured 0.4 % slower: opt-in
 
 
 def _add_ln(h: torch.Tensor, x: torch.Tensor, norm: nn.LayerNorm):
     """(h + x, LayerNorm(h + x)) in one K8 pass; h is overwritten with the sum."""
-    if not _FUSE_ADD_LN or not h.is_contiguous() or h.shape != x.shape or not x.is_contiguous():
+    if not h.is_contiguous() or h.shape != x.shape or not x.is_contiguous():
         s = h + x
         return s, layer_norm(norm, s)
     return ops.add_layer_norm(h, x, norm.weight, norm.bias, norm.eps)
@@ -217,7 +213,7 @@ class GEGLU(nn.Module):
 
         # measured per shape: K10 wins where K is small (res-64, K = 320), hipBLASLt's GEMM elsewhere
         key = ("geglu", tuple(x.shape), tuple(self.proj.weight.shape))
-        ok = _FUSE_GEGLU and ops.linear_geglu_supported(x, self.proj.weight)
+        ok = ops.linear_geglu_supported(x, self.proj.weight)
         return fused() if ops.CONV.pick(key, ok, fused, unfused) else unfused()
 
     def _interleaved(self):
@@ -274,23 +270,15 @@ class BasicTransformerBlock(nn.Module):
             x = self.ff(layer_norm(self.norm3, x)) + x
             x = self.attn_temp(layer_norm(self.norm_temp, x), video_length=frames, temporal_layout="bf") + x
             return x
-        # inference: each residual add rides on the output projection's K10 epilogue where K10 runs
-        # that projection (the next LayerNorm then reads one tensor instead of two and writes one),
-        # otherwise on the next LayerNorm (K8 + add); the same two roundings either way
-        C = x.shape[-1]
-        M = x.numel() // C
-        if _FUSE_OUT_RES and x.is_contiguous() and ops.linear_add_fused(M, C, C) and ops.linear_add_fused(M, 4 * C, C):
-            x = self.attn1(layer_norm(self.norm1, x), video_length=frames, residual=x)
-            x = self.attn2(layer_norm(self.norm2, x), encoder_hidden_states=context, video_length=frames, residual=x)
-            x = self.ff(layer_norm(self.norm3, x), residual=x)
-            y = layer_norm(self.norm_temp, x)
-        else:
-            h = self.attn1(layer_norm(self.norm1, x), video_length=frames)
-            x, y = _add_ln(h, x, self.norm2)
-            h = self.attn2(y, encoder_hidden_states=context, video_length=frames)
-            x, y = _add_ln(h, x, self.norm3)
-            h = self.ff(y)
-            x, y = _add_ln(h, x, self.norm_temp)
+        # inference: each residual add rides on the next LayerNorm (K8 + add: it reads h and x, writes
+        # the sum and the normed sum).  (Adding in the output projections' K10 epilogue instead, same
+        # roundings, measured 0.4 % slower end to end: profiles/r03_fuse_out_res_rejected.jsonl.)
+        h = self.attn1(layer_norm(self.norm1, x), video_length=frames)
+        x, y = _add_ln(h, x, self.norm2)
+        h = self.attn2(y, encoder_hidden_states=context, video_length=frames)
+        x, y = _add_ln(h, x, self.norm3)
+        h = self.ff(y)
+        x, y = _add_ln(h, x, self.norm_temp)
         # the last residual add rides on attn_temp's output projection (fused where it measures faster)
         return self.attn_temp(y, video_length=frames, temporal_layout="bf", residual=x)
 
@@ -446,7 +434,6 @@ class UpBlock3D(_UpBlock):
         self.attentions = None
 
 
-_T_CACHE = os.environ.get("VP2P_T_CACHE", "1") != "0"     # A/B switch (0: a new H2D copy per forward)
 
 
 class UNet3DConditionModel(nn.Module):
@@ -505,7 +492,7 @@ class UNet3DConditionModel(nn.Module):
             # torch.tensor(..., device=cuda) is a blocking H2D copy that drains the stream every step
             tc = self.__dict__.setdefault("_t_dev", {})
             key = (int(t), sample.device)
-            if key not in tc or not _T_CACHE:
+            if key not in tc:
                 tc[key] = torch.tensor([int(t)], dtype=torch.int64, device=sample.device)
             t = tc[key]
         elif t.dim() == 0:
