@@ -56,6 +56,38 @@ def test_shared_kv_attention_backward(dt, d, frames, N, Nk):
     assert _rel(kvc.grad[..., C:], kvr.grad[..., C:]) < tol, _rel(kvc.grad[..., C:], kvr.grad[..., C:])
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("N,d", [(4096, 40), (1024, 80), (256, 160)])
+def test_shared_kv_attention_backward_real_size(dt, N, d):
+    """K1b at the UNet's real sizes (VERDICT r03 "backward at real size"): 8 frames x N query tokens
+    against the N frame-0 keys -- the res-64 / res-32 / res-16 layers of configs[3] (8 frames at 512^2),
+    where every dK / dV row sums 8 N query rows.  Reference: fp32 torch autograd of the same math, on
+    the GPU (the (heads, 8N, N) score tensor is 1 GiB at res-64).  Full dQ, dK and dV compared."""
+    from vp2p import autograd
+    dtype, tol = DT[dt]
+    tol = 1e-3 if dt == "fp32" else tol
+    heads, B, frames = 2, 1, 8
+    C = heads * d
+    g = torch.Generator().manual_seed(N + d)
+    q = torch.randn(B * frames, N, C, generator=g).to(dtype)
+    kv = torch.randn(B, N, 2 * C, generator=g).to(dtype)
+    dout = torch.randn(B * frames, N, C, generator=g).to(dtype)
+    scale = d ** -0.5
+    qr = q.detach().cuda().float().requires_grad_()
+    kvr = kv.detach().cuda().float().requires_grad_()
+    ref, _ = _ref_shared(qr, kvr, frames, heads, scale)
+    ref.backward(dout.cuda().float())
+    qc, kvc = q.detach().cuda().requires_grad_(), kv.detach().cuda().requires_grad_()
+    out = autograd.SharedKVAttention.apply(qc, kvc, frames, heads, scale)
+    out.backward(dout.cuda())
+    torch.cuda.synchronize()
+    assert _rel(out, ref.detach()) < tol, _rel(out, ref.detach())
+    assert _rel(qc.grad, qr.grad) < tol, _rel(qc.grad, qr.grad)
+    assert _rel(kvc.grad[..., :C], kvr.grad[..., :C]) < tol, _rel(kvc.grad[..., :C], kvr.grad[..., :C])
+    assert _rel(kvc.grad[..., C:], kvr.grad[..., C:]) < tol, _rel(kvc.grad[..., C:], kvr.grad[..., C:])
+
+
 def test_frame_attention_lse():
     from vp2p import ops
     heads, d, B, f, N, Nk = 2, 40, 1, 2, 96, 200

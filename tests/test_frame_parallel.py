@@ -280,3 +280,94 @@ def test_frame_sharded_nulltext_matches_single(tmp_path):
         diff = (torch.cat(got["unc"]) - torch.cat([u.cpu() for u in unc])).abs()
         # Adam's sqrt(v) normalisation: near-zero-gradient elements move by a fraction of lr (1e-2)
         assert float(diff.mean()) < 1e-3 and float(diff.max()) < 2.5e-2, (float(diff.mean()), float(diff.max()))
+
+
+# ------------------------------------------------------------------------------------------------
+def _penguin_worker(rank, world, port, out_path):
+    """configs[2] (penguin-run refine edit, 24 frames, SD-1.5 geometry, bf16) under the bench's
+    4-rank EditLayout: CFG split x 2 frame shards of 12 frames each (all ranks on the one GPU, gloo
+    with host staging).  The reference fixture's 12 saved steps are what it is compared against."""
+    dist = _init(rank, world, port)
+    import model_spec as MS
+    import spec
+    import vp2p
+    from vp2p.frame_parallel import EditLayout, frame_parallel
+    from vp2p.pipeline import VideoP2PPipeline
+    from vp2p.tokenizer import SyntheticCLIPTokenizer
+    from vp2p.unet3d import UNet3DConditionModel, init_random_
+    edit, f, steps, save = MS.EDITS["penguin24"]
+    prompts, swap, blend, eq, cross, self_ = spec.CONFIGS[edit]
+    tok = SyntheticCLIPTokenizer()
+    state = init_random_(UNet3DConditionModel(), seed=0).state_dict()
+    unet = UNet3DConditionModel()
+    unet.load_state_dict(MS.edit_state(state), strict=True)
+    del state
+    unet = unet.to("cuda", torch.bfloat16).to(memory_format=torch.channels_last).eval()
+    ctrl = vp2p.make_controller(prompts, swap, {"default_": cross}, self_, ((blend[0],), (blend[1],)), eq,
+                                tokenizer=tok)
+    vp2p.register_attention_control(type("M", (), {"unet": unet})(), ctrl)
+    inp = MS.edit_inputs("penguin24", MS.blend_token_ids(prompts, blend, tok))
+    lay = EditLayout()
+    pipe = VideoP2PPipeline(unet)
+    pipe.keep_blend_mask = True
+    out = {"cur_step": None}
+
+    class Stop(Exception):
+        pass
+
+    def cb(i, t, lat):
+        if i in save:
+            out[f"lat/{i}"] = lay.frames.gather(lat, 2).cpu()
+            if ctrl.local_blend.counter > ctrl.local_blend.start_blend:
+                out[f"mask/{i}"] = lay.frames.gather(pipe.blend_mask.float(), 1).cpu().bool()
+        if i == steps - 1:
+            raise Stop
+
+    with torch.no_grad(), frame_parallel(lay):
+        try:
+            pipe(prompts, lay.frames_local(f), latents=lay.local(torch.from_numpy(inp["x_t"]).cuda(), 2),
+                 controller=ctrl, fast=True, text_embeddings=torch.from_numpy(inp["emb"]).cuda(),
+                 num_inference_steps=50, callback=cb)
+        except Stop:
+            pass
+    out["cur_step"] = ctrl.cur_step
+    out["lb_counter"] = ctrl.local_blend.counter
+    torch.save(out, out_path + f".{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_sharded_penguin24_vs_reference(tmp_path):
+    """SURVEY §8(e) at a real configuration: the 4-rank layout (CFG split x 2 frame shards) of the
+    24-frame penguin refine edit against the reference pipeline's fixture (golden_edit_penguin24.npz,
+    12 of 50 steps).  Bar: the bf16 end-to-end bar, final-latent PSNR >= 45 dB; the LocalBlend mask
+    flips against the reference are reported (bf16: informational, as for the single-rank case)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import model_spec as MS
+    from conftest import record
+    path = os.path.join(ROOT, "tests", "golden", "golden_edit_penguin24.npz")
+    if not os.path.exists(path):
+        pytest.skip("golden_edit_penguin24.npz not generated")
+    gold = np.load(path)
+    out = str(tmp_path / "penguin")
+    mp.spawn(_penguin_worker, args=(4, _port(), out), nprocs=4, join=True)
+    _, f, steps, save = MS.EDITS["penguin24"]
+    for r in range(4):
+        got = torch.load(out + f".{r}")
+        assert got["cur_step"] == int(gold["cur_step"]) and got["lb_counter"] == int(gold["lb_counter"]), r
+        report = []
+        for i in save:
+            a = got[f"lat/{i}"].numpy().astype(np.float64)
+            ref = gold[f"latents/{i}"].astype(np.float64)
+            p = float(10 * np.log10((ref ** 2).max() / max(((a - ref) ** 2).mean(), 1e-30)))
+            report.append((i, round(p, 1)))
+            if f"mask/{i}" in gold.files and f"mask/{i}" in got:
+                m = got[f"mask/{i}"].numpy()
+                ref_mask = np.unpackbits(gold[f"mask/{i}"])[: m.size].reshape(m.shape).astype(bool)
+                report.append((i, "mask flips", int((m != ref_mask).sum()), m.size))
+        if r == 0:
+            record("edit/penguin24-sharded-4rank/bf16", steps=report)
+        last = report[[k for k, x in enumerate(report) if len(x) == 2][-1]][1]
+        assert last >= 45.0, (r, report)

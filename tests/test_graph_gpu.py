@@ -28,6 +28,7 @@ def test_graphed_edit_bit_equal(tokenizer):
     pipe, ctrl, prompts, emb = _edit_setup(tokenizer)
     steps = 14          # crosses the cross-replace (10) and LocalBlend (counter > 10) edges
     outs = {}
+    entries = None
     for seed in (2, 3):
         x_t = torch.randn(1, 4, 2, 64, 64, generator=torch.Generator().manual_seed(seed)).cuda()
         with torch.no_grad():
@@ -43,6 +44,30 @@ def test_graphed_edit_bit_equal(tokenizer):
         assert torch.isfinite(eager).all()
         assert torch.equal(eager, graphed), float((eager - graphed).abs().max())
         outs[seed] = graphed
-    # the second seed replayed the graphs captured for the first (one cache entry)
-    assert len(pipe._graph_cache) == 1
+        entries = entries if seed == 3 else pipe._graph_cache[1]
+    # the second seed replayed the graphs captured for the first (the same cache entry)
+    assert pipe._graph_cache[1] is entries
     assert not torch.equal(outs[2], outs[3])
+
+
+@pytest.mark.timeout(300)
+def test_graphed_edits_new_controller_memory_bounded(tokenizer):
+    """a session that builds a controller per edit keeps ONE captured edit: the previous
+    edit's graphs, pool and controller are released, so device memory does not grow edit after edit."""
+    import bench
+    import vp2p
+    pipe, ctrl, prompts, emb = _edit_setup(tokenizer)
+    prompts, swap, blend, eq, cross, self_ = bench.RABBIT
+    x_t = torch.randn(1, 4, 2, 64, 64, generator=torch.Generator().manual_seed(2)).cuda()
+    used = []
+    for k in range(3):
+        c = vp2p.make_controller(prompts, swap, {"default_": cross}, self_, blend, eq, tokenizer=tokenizer)
+        vp2p.register_attention_control(type("M", (), {"unet": pipe.unet})(), c)
+        with torch.no_grad():
+            pipe(prompts, 2, latents=x_t, controller=c, fast=True, text_embeddings=emb, num_inference_steps=4,
+                 graphs=True)
+        del c
+        torch.cuda.synchronize()
+        used.append(torch.cuda.memory_allocated())
+    assert pipe._graph_cache[1].controller is not None
+    assert used[2] <= used[0] + (64 << 20), used

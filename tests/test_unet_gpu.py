@@ -67,6 +67,23 @@ def test_unet_forward_matches_oracle(tokenizer, dtype, tol, name, step):
     assert np.abs(got_lb - ref_lb).max() / np.abs(ref_lb).max() < tol
 
 
+def test_unet_forward_inference_mode(tokenizer):
+    """a forward under torch.inference_mode() (inference tensors have no version counter,
+    so the context / K|V caches must not key on one) equals the no_grad forward, twice in a row."""
+    unet, sd, ctrl, octrl = _setup(tokenizer, "rabbit", torch.bfloat16)
+    x, ctx = _inputs(5)
+    x, ctx = x.cuda().bfloat16(), ctx.cuda().bfloat16()
+    with torch.no_grad():
+        ctrl.cur_step = 0
+        ref = unet(x, 981, ctx).sample.clone()
+    for _ in range(2):
+        with torch.inference_mode():
+            ctrl.cur_step = 0
+            xi, ci = x.clone(), ctx.clone()       # inference tensors
+            got = unet(xi, 981, ci).sample
+        assert torch.equal(got, ref), float((got.float() - ref.float()).abs().max())
+
+
 @pytest.mark.parametrize("substruct", [None, "grass"])
 def test_edit_loop_fast_mode(tokenizer, substruct):
     """Three denoising steps through the pipeline (fused CFG + DDIM + LocalBlend) vs the oracle,

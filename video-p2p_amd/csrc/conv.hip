@@ -75,11 +75,6 @@ constexpr int GBM = 128, NW = 4;                               // the split-K / 
 //  2: 256 x 320 "wide", 8 waves (2 x 4 of 128 x 80: 8 x 5 MFMA tiles, every A fragment used 5x,
 //     every B fragment 8x), two stages (2 x 72 KB), one workgroup per CU: twice the MFMAs per LDS
 //     byte read and per barrier of 0 / 1 (Cout % 320 == 0; the epilogue runs in two 128-row passes);
-//  3: the wide tile on 32-channel K-steps in a FOUR-stage ring (4 x 36 KB): the DMA of three steps in
-//     flight under the MFMAs of one (counted vmcnt + raw s_barrier), where the two-stage wide tile
-//     issues a step's DMA only one step ahead.  64-byte LDS rows; LDS slot j of row r holds global
-//     chunk j ^ S[(r >> 2) & 3], S = {0, 2, 3, 1}: the 16 rows of each 16-lane ds_read_b128 group
-//     (rows 0-15 once, chunks c or c + 1) then hit 16 distinct 4-bank groups.
 // All: the same per-output K order and MFMA sequence (one 16x16x32 MFMA per 32 channels), so
 // bit-equal results.
 template <int TBM_, int TBN_, int WTM_, int NST_, int KB_ = 64> struct GTile {

@@ -35,6 +35,9 @@
 #ifndef VP2P_K1_PP_WAVES
 #define VP2P_K1_PP_WAVES 4
 #endif
+#ifndef VP2P_K1_PP_POLY
+#define VP2P_K1_PP_POLY 0
+#endif
 
 namespace vp2p {
 
@@ -66,6 +69,25 @@ __device__ __forceinline__ bf16x4 ldtr(const lchar* p) {
 //  * v_cvt -> PV MFMA reading the packed P: one whole block apart;
 //  * VALU write of P / O in the rare rescale -> MFMA: the s_nop 1 opening every block;
 //  * PV MFMA -> VALU read of O: o_fence() (two s_nop 7).
+// 2^x of a pair on the plain VALU pipe (packed f32): t = x + 1.5*2^23 holds n = round(x) in its low
+// bits, f = x - n in [-0.5, 0.5], 2^f by the degree-2 minimax polynomial (relative error 1.7e-3,
+// under the half-ulp 3.9e-3 of the bf16 the result is rounded to), and n added into the exponent
+// field.  x is clamped at -126 so the exponent cannot wrap (2^-126 underflows to 0 in the bf16 P
+// anyway whenever it matters: P is normalised by a row sum >= 1).
+__device__ __forceinline__ f32x2 pexp2(f32x2 x) {
+  x[0] = fmaxf(x[0], -126.f);
+  x[1] = fmaxf(x[1], -126.f);
+  const f32x2 M = {12582912.f, 12582912.f};
+  const f32x2 t = x + M;
+  const f32x2 f = x - (t - M);
+  const f32x2 p = (f * f32x2{0.23842894f, 0.23842894f} + f32x2{0.70344818f, 0.70344818f}) * f +
+                  f32x2{1.0004431f, 1.0004431f};
+  f32x2 y;
+  y[0] = __uint_as_float(__float_as_uint(p[0]) + (__float_as_uint(t[0]) << 23));
+  y[1] = __uint_as_float(__float_as_uint(p[1]) + (__float_as_uint(t[1]) << 23));
+  return y;
+}
+
 __device__ __forceinline__ uint32_t vcvt(float x, float y) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x, y}, bf16x2));
 }
@@ -93,7 +115,7 @@ __device__ __forceinline__ void pv(f32x16& o, const bf16x8& v, const u32x4& p) {
 
 }  // namespace
 
-template <int SETS, int WAVES>
+template <int SETS, int WAVES, int POLY>
 __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(const vp2p_frame_attn_args a) {
   static_assert(SETS >= 2, "the QK^T of the last set rides in group 0 of the next block");
   static_assert(WAVES == 4 || WAVES == 8, "one or two waves per SIMD");
@@ -264,46 +286,59 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(co
       uint32_t pn[8];
       f32x16 acc;
       const f32x16& sg = S[g];
-      // slot 0: exps 0-2 | QK k-step 0
-      e[0] = fast_exp2(sg[0]); e[1] = fast_exp2(sg[1]); e[2] = fast_exp2(sg[2]);
+      // pair k = scores 2k, 2k+1: two v_exp, or (bit k of POLY) one packed polynomial on the plain
+      // VALU pipe, which leaves the transcendental unit to the other pairs
+      auto pair = [&](int k) {
+        if ((POLY >> k) & 1) {
+          const f32x2 y = pexp2(f32x2{sg[2 * k], sg[2 * k + 1]});
+          e[2 * k] = y[0];
+          e[2 * k + 1] = y[1];
+        } else {
+          e[2 * k] = fast_exp2(sg[2 * k]);
+          e[2 * k + 1] = fast_exp2(sg[2 * k + 1]);
+        }
+      };
+      // slot 0: pair 0 | QK k-step 0
+      pair(0);
       qk_first(acc, kf[0], qf[qs][0]);
       if (g == 0) kf[0] = ld128(kb + krow * kRowB);
       sb();
-      // slot 1: cvt 0-1, exps 3-4 | PV(sp 0, tile 1)
-      pn[0] = vcvt(e[0], e[1]);
-      e[3] = fast_exp2(sg[3]); e[4] = fast_exp2(sg[4]);
+      // slot 1: pair 1 | PV(sp 0, tile 1) | cvt pair 0
+      pair(1);
       pv<OA>(o[g][1], vf[0][1], P[g][0]);
+      pn[0] = vcvt(e[0], e[1]);
       if (last) vf[0][1] = v_tr(0, 1);
       sb();
-      // slot 2: cvt 2-3, exps 5-6 | QK k-step 1
-      pn[1] = vcvt(e[2], e[3]);
-      e[5] = fast_exp2(sg[5]); e[6] = fast_exp2(sg[6]);
+      // slot 2: pair 2 | QK k-step 1 | cvt pair 1
+      pair(2);
       qk_next(acc, kf[1], qf[qs][1]);
+      pn[1] = vcvt(e[2], e[3]);
       if (g == 0) kf[1] = ld128(kb + krow * kRowB + 32);
       sb();
-      // slot 3: cvt 4-5, exps 7-8 | PV(sp 0, tile 0)
-      pn[2] = vcvt(e[4], e[5]);
-      e[7] = fast_exp2(sg[7]); e[8] = fast_exp2(sg[8]);
+      // slot 3: pair 3 | PV(sp 0, tile 0) | cvt pair 2
+      pair(3);
       pv<OA>(o[g][0], vf[0][0], P[g][0]);
+      pn[2] = vcvt(e[4], e[5]);
       if (last) vf[0][0] = v_tr(0, 0);
       sb();
-      // slot 4: cvt 6-7, exps 9-10 | QK k-step 2 -> S[qs]
-      pn[3] = vcvt(e[6], e[7]);
-      e[9] = fast_exp2(sg[9]); e[10] = fast_exp2(sg[10]);
+      // slot 4: pair 4 | QK k-step 2 -> S[qs] | cvt pair 3
+      pair(4);
       qk_next(acc, kf[2], qf[qs][2]);
+      pn[3] = vcvt(e[6], e[7]);
       if (g == 0) kf[2] = ld128(k2b + krow * kRowB + 64);
       sb();
-      // slot 5: cvt 8-9, exps 11-13 | PV(sp 1, tile 1)
-      pn[4] = vcvt(e[8], e[9]);
-      e[11] = fast_exp2(sg[11]); e[12] = fast_exp2(sg[12]); e[13] = fast_exp2(sg[13]);
+      // slot 5: pair 5 | PV(sp 1, tile 1) | cvt pair 4
+      pair(5);
       pv<OA>(o[g][1], vf[1][1], P[g][1]);
+      pn[4] = vcvt(e[8], e[9]);
       if (last) vf[1][1] = v_tr(1, 1);
       sb();
-      // slot 6: cvt 10-13, exps 14-15 | PV(sp 1, tile 0) | cvt 14-15
+      // slot 6: pairs 6-7 | PV(sp 1, tile 0) | cvt pairs 5-7
+      pair(6);
+      pair(7);
+      pv<OA>(o[g][0], vf[1][0], P[g][1]);
       pn[5] = vcvt(e[10], e[11]);
       pn[6] = vcvt(e[12], e[13]);
-      e[14] = fast_exp2(sg[14]); e[15] = fast_exp2(sg[15]);
-      pv<OA>(o[g][0], vf[1][0], P[g][1]);
       pn[7] = vcvt(e[14], e[15]);
       if (last) vf[1][0] = v_tr(1, 0);
       S[qs] = acc;
@@ -427,7 +462,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(co
 }
 
 int launch_frame_attn_pp(const vp2p_frame_attn_args* a, hipStream_t stream) {
-  constexpr int SETS = VP2P_K1_PP_SETS, WAVES = VP2P_K1_PP_WAVES;
+  constexpr int SETS = VP2P_K1_PP_SETS, WAVES = VP2P_K1_PP_WAVES, POLY = VP2P_K1_PP_POLY;
   if (a->dtype != VP2P_BF16 || a->head_dim != kD || !a->q_prescaled || a->tokens_kv % kKT) return VP2P_E_SHAPE;
   // 32-bit buffer offsets: every key row of one (b, head) within 4 GiB
   if ((int64_t)a->tokens_kv * a->k_sn * 2 >= (1ll << 32) || (int64_t)a->tokens_kv * a->v_sn * 2 >= (1ll << 32))
@@ -435,10 +470,10 @@ int launch_frame_attn_pp(const vp2p_frame_attn_args* a, hipStream_t stream) {
   const int FQ = a->frames * a->tokens_q;
   const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 32 * SETS * WAVES - 1) / (32 * SETS * WAVES));
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_pp<SETS, WAVES>),
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_pp<SETS, WAVES, POLY>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  hipLaunchKernelGGL((frame_attn_kernel_pp<SETS, WAVES>), dim3((unsigned)nwg), dim3(64 * WAVES), kLdsBytes, stream, *a);
+  hipLaunchKernelGGL((frame_attn_kernel_pp<SETS, WAVES, POLY>), dim3((unsigned)nwg), dim3(64 * WAVES), kLdsBytes, stream, *a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 

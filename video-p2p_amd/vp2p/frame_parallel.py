@@ -20,8 +20,11 @@ attention.py:296-302           FrameAttention reads frame 0's K/V          frame
                                                                            broadcast; every rank projects K|V
 resnet.py:142,158; unet.py:206 5-D GroupNorm statistics over (c/G, f, h, w) all-gather of the K7 per-chunk
                                                                            (count, mean, M2) partials
-attention.py:262-268           attn_temp attends over all f frames         all-to-all frames <-> tokens,
-                                                                           before and after the kernel
+attention.py:262-268           attn_temp attends over all f frames         all-to-all frames <-> tokens of
+                                                                           the normed hidden state (C per
+                                                                           token; q|k|v projected after it)
+                                                                           and of the output, in token
+                                                                           pieces overlapped with the kernel
 =============================  ==========================================  =================================
 
 Backward (the null-text optimisation, run_videop2p.py:580-612, frame-sharded): each collective has
