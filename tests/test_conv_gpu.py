@@ -63,6 +63,24 @@ def test_conv2d_large_m(n, cin, h, w, cout, k, stride, residual):
     _case(n, cin, h, w, cout, k, stride, residual=residual, seed=3)
 
 
+@pytest.mark.parametrize("n,cin,h,w,cout,k,residual", [
+    (4, 320, 64, 64, 320, 3, False),         # 1-frame edit (B 4) res-64: 256 128-row tiles -> 512 64-row
+    (8, 640, 32, 32, 640, 3, True),          # 2-frame res-32 + residual
+    (4, 960, 64, 64, 320, 1, False),         # conv_shortcut 1x1
+    (5, 320, 51, 53, 320, 3, True),          # ragged last 64-row tile
+])
+def test_conv2d_short_tile(n, cin, h, w, cout, k, residual):
+    """The 64 x 160 tile (small clips whose 128-row grid leaves CUs idle): one pass, no split-K
+    workspace, against the fp32 reference."""
+    from vp2p import ops, _lib
+    import ctypes
+    _case(n, cin, h, w, cout, k, 1, residual=residual, seed=4)
+    x = torch.empty(n, cin, h, w, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = torch.empty(cout, cin, k, k, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a, _ = ops._conv_args(x, wt, None, None, None, 1, (k - 1) // 2)
+    assert _lib.load().vp2p_conv2d_workspace_bytes(ctypes.byref(a)) == 0
+
+
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv2d_residual(k):
     _case(2, 640, 8, 8, 640, k, 1, residual=True, seed=1)
@@ -109,7 +127,8 @@ def test_conv2d_unsupported_raises():
         ops.conv2d(x, wt, None, 1, 1)
 
 
-@pytest.mark.parametrize("M,K,inner", [(1000, 320, 1280), (257, 640, 2560), (64, 1280, 5120), (65536 + 77, 320, 1280)])
+@pytest.mark.parametrize("M,K,inner", [(1000, 320, 1280), (257, 640, 2560), (64, 1280, 5120), (65536 + 77, 320, 1280),
+                                        (1600, 320, 1280)])
 def test_linear_geglu(M, K, inner):
     """K10 with the GEGLU epilogue vs F.linear + diffusers GEGLU in fp32 on the same bf16 inputs
     (projection rounded to bf16, gelu rounded, product rounded -- torch's eager roundings)."""

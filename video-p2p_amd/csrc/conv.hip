@@ -75,6 +75,8 @@ constexpr int GBM = 128, NW = 4;                               // the split-K / 
 //  2: 256 x 320 "wide", 8 waves (2 x 4 of 128 x 80: 8 x 5 MFMA tiles, every A fragment used 5x,
 //     every B fragment 8x), two stages (2 x 72 KB), one workgroup per CU: twice the MFMAs per LDS
 //     byte read and per barrier of 0 / 1 (Cout % 320 == 0; the epilogue runs in two 128-row passes);
+//  3: 64 x 160 "short", 4 waves (2 x 2 of 32 x 80), two stages: the small-clip shapes whose 128-row
+//     grid would leave CUs idle (1-2 frame edits), one pass where 0 needed a split-K second pass;
 // All: the same per-output K order and MFMA sequence (one 16x16x32 MFMA per 32 channels), so
 // bit-equal results.
 template <int TBM_, int TBN_, int WTM_, int NST_, int KB_ = 64> struct GTile {
@@ -103,6 +105,7 @@ template <int CF> struct GCfg;
 template <> struct GCfg<0> : GTile<128, 160, 4, 2> {};
 template <> struct GCfg<1> : GTile<256, 160, 4, 3> {};
 template <> struct GCfg<2> : GTile<256, 320, 8, 2> {};
+template <> struct GCfg<3> : GTile<64, 160, 2, 2> {};
 constexpr int G_STAGE = GCfg<0>::STAGE;
 constexpr int G_LDS = GCfg<0>::LDS;
 
@@ -334,8 +337,13 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   int cur = 0;                                    // LDS stage of this step
   for (int step = s_begin; step < s_end; ++step) {
     if constexpr (Cfg::NSTAGE == 2) {
+#ifndef VP2P_K10_DIAG
       __syncthreads();                            // vmcnt(0): step's DMA landed; step-1's reads done
       if (step + 1 < s_end) dma(step + 1, cur ^ 1);
+#else   // lab diagnostics only (wrong results): 1 = no main-loop DMA, 3 = no DMA and no barrier
+      if (!(VP2P_K10_DIAG & 2)) __syncthreads();
+      if (!(VP2P_K10_DIAG & 1) && step + 1 < s_end) dma(step + 1, cur ^ 1);
+#endif
     } else {
       // this wave's DMA of `step` landed (the ones of the next steps may stay in flight: in-order
       // vmcnt), then every wave's: the barrier also orders all reads of stage (step - 1) % NSTAGE
@@ -485,6 +493,11 @@ __global__ __launch_bounds__(512, 1) void conv_kernel_w(const vp2p_conv_args a) 
   conv_tile<KS, EPI, AM, 2>(a);
 }
 
+template <int KS, int EPI = 0, int AM = 1>
+__global__ __launch_bounds__(256, 2) void conv_kernel_s(const vp2p_conv_args a) {
+  conv_tile<KS, EPI, AM, 3>(a);
+}
+
 template <int KS, int EPI, int AM, int CF> struct ConvKernel;
 template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 0> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_g<KS, EPI, AM>); }
@@ -494,6 +507,9 @@ template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 1> {
 };
 template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 2> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_w<KS, EPI, AM>); }
+};
+template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 3> {
+  static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_s<KS, EPI, AM>); }
 };
 
 // split-K second pass: y = round(round(sum_s ws[s] + bias) + residual), the one-pass roundings
@@ -537,8 +553,10 @@ static int launch_g1(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL((conv_kernel_g<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   else if constexpr (CF == 1)
     hipLaunchKernelGGL((conv_kernel_b<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
-  else
+  else if constexpr (CF == 2)
     hipLaunchKernelGGL((conv_kernel_w<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
+  else
+    hipLaunchKernelGGL((conv_kernel_s<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
@@ -570,10 +588,23 @@ static int pick_tile(const vp2p_conv_args* a, int64_t M) {
   return (tiles_b >= 256 && a->kernel == 1 && a->cin >= 1280) ? 1 : 0;
 }
 
+// the 64-row tile: where the 128-row grid leaves CUs idle (< 384 tiles) and the 64-row one gives
+// at least kShortMin tiles
+#ifndef VP2P_CONV_SHORT_MIN
+#define VP2P_CONV_SHORT_MIN 384
+#endif
+constexpr int64_t kShortMin = VP2P_CONV_SHORT_MIN;
+static bool short_tile(const vp2p_conv_args* a, int64_t M) {
+  const int64_t tiles = (M + GBM - 1) / GBM * (a->cout / BN);
+  const int64_t tiles_s = (M + 63) / 64 * (a->cout / BN);
+  return tiles < 384 && tiles_s >= kShortMin;
+}
+
 // K-split for this shape: 1 unless the grid would leave most CUs idle (the 8x8-latent convs)
 static int pick_ksplit(const vp2p_conv_args* a) {
   if (a->epilogue != VP2P_CONV_EPI_NONE) return 1;
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
+  if (short_tile(a, M)) return 1;
   const int64_t tiles = (M + GBM - 1) / GBM * (a->cout / BN);
   const int nsteps = a->kernel * a->kernel * (a->cin / BK);
   if (tiles >= 384) return 1;
@@ -647,6 +678,10 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
     if (rc != VP2P_OK) return rc;
     const int64_t n = M * (a->cout / 8);
     hipLaunchKernelGGL(conv::conv_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
+  } else if (conv::short_tile(a, M)) {
+    const dim3 gs((unsigned)((M + 63) / 64 * (a->cout / conv::BN)));
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 3>(*a, gs, fast, s);
+    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 3>(*a, gs, fast, s) : conv::launch_g<1, 0, 3>(*a, gs, fast, s);
   } else if (const int cf = conv::pick_tile(a, M); cf == 1) {
     const dim3 gb((unsigned)((M + 255) / 256 * (a->cout / conv::BN)));
     if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 1>(*a, gb, fast, s);
