@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 13
+#define VP2P_ABI_VERSION 14
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -279,6 +279,13 @@ int vp2p_group_norm_finalize(const vp2p_group_norm_args* args, const float* part
                              float* stats, void* stream);
 /* The apply of vp2p_group_norm_apply on finalized statistics. */
 int vp2p_group_norm_apply_stats(const vp2p_group_norm_args* args, const float* stats, void* stream);
+/* Frame-sharded callers: merge this rank's partial array into one (count, mean, M2) triple per
+ * (batch, group), fp32 (batch, groups, 3) -- what the ranks exchange (B*G*12 bytes instead of the
+ * B*parts*G*12 of the raw partials) -- and, after the gather, finalize nsets such triple arrays laid
+ * out back to back into {mean, rstd} (batch, groups, 2) for vp2p_group_norm_apply_stats. */
+int vp2p_group_norm_merge(const vp2p_group_norm_args* args, const float* partials, float* triples, void* stream);
+int vp2p_group_norm_finalize_merged(const vp2p_group_norm_args* args, const float* triples, int32_t nsets,
+                                    float* stats, void* stream);
 
 /* ---- K8: LayerNorm over the channel axis --------------------------------------------------------
  * nn.LayerNorm of BasicTransformerBlock.norm1/norm2/norm3/norm_temp (attention.py:200-216). */

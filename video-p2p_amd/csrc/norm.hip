@@ -211,7 +211,9 @@ __global__ __launch_bounds__(512) void gn_stats_kernel(const vp2p_group_norm_arg
 }
 
 // Finalize: one 256-thread block per (group, batch element) merges that group's nsets x parts
-// partials -- one load per thread in flight, then a fixed-order tree in LDS -- into {mean, rstd}.
+// partials -- one load per thread in flight, then a fixed-order tree in LDS -- into {mean, rstd}
+// (TRIPLE: into the merged (count, mean, M2), the frame-sharded exchange).
+template <bool TRIPLE = false>
 __global__ __launch_bounds__(256) void gn_finalize_kernel(const vp2p_group_norm_args a, const GnGeom g,
                                                           const float* __restrict__ partials, int nsets,
                                                           float* __restrict__ stats) {
@@ -238,8 +240,15 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const vp2p_group_norm_
     __syncthreads();
   }
   if (tid == 0) {
-    stats[((int64_t)b * G + gi) * 2] = s_mean[0];
-    stats[((int64_t)b * G + gi) * 2 + 1] = rsqrtf(s_m2[0] / s_n[0] + a.eps);
+    if constexpr (TRIPLE) {
+      float* o = stats + ((int64_t)b * G + gi) * 3;
+      o[0] = s_n[0];
+      o[1] = s_mean[0];
+      o[2] = s_m2[0];
+    } else {
+      stats[((int64_t)b * G + gi) * 2] = s_mean[0];
+      stats[((int64_t)b * G + gi) * 2 + 1] = rsqrtf(s_m2[0] / s_n[0] + a.eps);
+    }
   }
 }
 
@@ -800,8 +809,31 @@ extern "C" int vp2p_group_norm_finalize(const vp2p_group_norm_args* a, const flo
   if (rc != VP2P_OK) return rc;
   if (!partials || !stats || nsets <= 0) return VP2P_E_ARG;
   if ((int64_t)nsets * g.parts >= ((int64_t)1 << 31)) return VP2P_E_SHAPE;
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(a->groups, a->batch), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     *a, g, partials, nsets, stats);
+  hipLaunchKernelGGL(gn_finalize_kernel<false>, dim3(a->groups, a->batch), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), *a, g, partials, nsets, stats);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_merge(const vp2p_group_norm_args* a, const float* partials, float* triples,
+                                     void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!partials || !triples) return VP2P_E_ARG;
+  hipLaunchKernelGGL(gn_finalize_kernel<true>, dim3(a->groups, a->batch), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), *a, g, partials, 1, triples);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_finalize_merged(const vp2p_group_norm_args* a, const float* triples, int32_t nsets,
+                                               float* stats, void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!triples || !stats || nsets <= 0) return VP2P_E_ARG;
+  g.parts = 1;                                          // one merged triple per (set, batch, group)
+  hipLaunchKernelGGL(gn_finalize_kernel<false>, dim3(a->groups, a->batch), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), *a, g, triples, nsets, stats);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 

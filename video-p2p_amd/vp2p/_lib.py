@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
@@ -29,7 +29,7 @@ EXPORTS = ("vp2p_frame_attn_fwd", "vp2p_cross_kv_workspace_bytes", "vp2p_cross_k
            "vp2p_group_norm_bwd_reduce", "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd",
            "vp2p_nulltext_loss", "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
            "vp2p_add_layer_norm_fwd", "vp2p_conv2d_workspace_bytes", "vp2p_group_norm_finalize",
-           "vp2p_group_norm_apply_stats")
+           "vp2p_group_norm_apply_stats", "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged")
 
 
 class GroupNormArgs(ctypes.Structure):
@@ -158,6 +158,8 @@ def load(path: str = None):
     lib.vp2p_group_norm_fwd.argtypes = [gn, c_void_p]
     lib.vp2p_group_norm_finalize.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p]
     lib.vp2p_group_norm_apply_stats.argtypes = [gn, c_void_p, c_void_p]
+    lib.vp2p_group_norm_merge.argtypes = [gn, c_void_p, c_void_p, c_void_p]
+    lib.vp2p_group_norm_finalize_merged.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p]
     lib.vp2p_layer_norm_fwd.argtypes = [POINTER(LayerNormArgs), c_void_p]
     lib.vp2p_geglu_fwd.argtypes = [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]
     lib.vp2p_frame_attn_bwd_workspace_bytes.argtypes = [POINTER(FrameAttnBwdArgs)]
@@ -183,7 +185,8 @@ def load(path: str = None):
                  "vp2p_frame_attn_bwd", "vp2p_temporal_attn_bwd", "vp2p_group_norm_bwd_reduce",
                  "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd", "vp2p_nulltext_loss",
                  "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
-                 "vp2p_add_layer_norm_fwd", "vp2p_group_norm_finalize", "vp2p_group_norm_apply_stats"):
+                 "vp2p_add_layer_norm_fwd", "vp2p_group_norm_finalize", "vp2p_group_norm_apply_stats",
+                 "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged"):
         getattr(lib, name).restype = c_int32
     if lib.vp2p_abi_version() != ABI_VERSION:
         raise Vp2pError(f"{p}: ABI version {lib.vp2p_abi_version()} != {ABI_VERSION}; rebuild")

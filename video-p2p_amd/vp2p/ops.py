@@ -463,8 +463,19 @@ def group_norm(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor],
     s = _stream()
     check(lib.vp2p_group_norm_stats(ctypes.byref(a), s), "vp2p_group_norm_stats")
     nsets = 1
+    if shard is not None and shard.world > 1 and not return_stats:
+        # frames sharded: each rank merges its own partials into one (count, mean, M2) per
+        # (batch, group) and the ranks exchange those (B*G*12 bytes, not B*parts*G*12)
+        tri = torch.empty((Bf // frames) * num_groups * 3, device=x.device, dtype=torch.float32)
+        check(lib.vp2p_group_norm_merge(ctypes.byref(a), _ptr(partials), _ptr(tri), s), "vp2p_group_norm_merge")
+        tri = shard.all_gather_flat(tri)
+        st = torch.empty((Bf // frames) * num_groups * 2, device=x.device, dtype=torch.float32)
+        check(lib.vp2p_group_norm_finalize_merged(ctypes.byref(a), _ptr(tri), shard.world, _ptr(st), s),
+              "vp2p_group_norm_finalize_merged")
+        check(lib.vp2p_group_norm_apply_stats(ctypes.byref(a), _ptr(st), s), "vp2p_group_norm_apply_stats")
+        return out
     if shard is not None and shard.world > 1:
-        partials = shard.all_gather_flat(partials)
+        partials = shard.all_gather_flat(partials)     # the backward re-reads every rank's partials
         nsets = shard.world
     if parts * nsets >= GN_FINALIZE_MIN_PARTS:
         # one finalize launch merges the partials into (mean, rstd) per (batch, group); the apply
