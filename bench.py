@@ -192,7 +192,7 @@ class AttnTimer:
             roof = {"bound": "mfma", "achieved": k1["tflops"], "peak": peak, "unit": "TFLOP/s",
                     "frac": round(k1["tflops"] / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                     "traffic_source": src, "algorithmic_bytes": k1["bytes_per_launch"],
-                    "kernel": "vp2p::frame_attn_kernel_x2f<40,128,true> (res-64 FrameAttention, folded max)",
+                    "kernel": "vp2p::frame_attn_kernel_pp<2,8> (res-64 FrameAttention, software-pipelined, folded max)",
                     "launches": sum(1 for ev in self.events["frame_attention"] if ev[2][1] == k1["tokens"]),
                     "avg_ms": k1["avg_ms"], "flops_per_launch": k1["flop_per_launch"], "shape": k1["shape"]}
         attn = {"mfma_util": round(tot_flop / (tot_ms / 1e3) / 1e12 / peak, 4),

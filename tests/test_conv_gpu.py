@@ -68,6 +68,7 @@ def test_conv2d_large_m(n, cin, h, w, cout, k, stride, residual):
     (8, 640, 32, 32, 640, 3, True),          # 2-frame res-32 + residual
     (4, 960, 64, 64, 320, 1, False),         # conv_shortcut 1x1
     (5, 320, 51, 53, 320, 3, True),          # ragged last 64-row tile
+    (4, 320, 32, 32, 640, 3, False),         # 256 short tiles on a short K (45 steps)
 ])
 def test_conv2d_short_tile(n, cin, h, w, cout, k, residual):
     """The 64 x 160 tile (small clips whose 128-row grid leaves CUs idle): one pass, no split-K

@@ -588,16 +588,15 @@ static int pick_tile(const vp2p_conv_args* a, int64_t M) {
   return (tiles_b >= 256 && a->kernel == 1 && a->cin >= 1280) ? 1 : 0;
 }
 
-// the 64-row tile: where the 128-row grid leaves CUs idle (< 384 tiles) and the 64-row one gives
-// at least kShortMin tiles
-#ifndef VP2P_CONV_SHORT_MIN
-#define VP2P_CONV_SHORT_MIN 384
-#endif
-constexpr int64_t kShortMin = VP2P_CONV_SHORT_MIN;
+// the 64-row tile where the 128-row grid leaves CUs idle (< 384 tiles) and the 64-row one fills
+// them: >= 384 tiles, or >= 256 on short K (<= 48 K-steps; longer K keeps split-K, which measured
+// faster there).  Small-clip shapes, profiles/r04_k10_short_tile.jsonl: 1-frame res-64 3x3
+// 56.2 -> 43.4 us, 2-frame res-32 3x3 (320 -> 640) 50.5 -> 35.2 us, M 4096 K 640 N 640 14.4 -> 10.0 us.
 static bool short_tile(const vp2p_conv_args* a, int64_t M) {
   const int64_t tiles = (M + GBM - 1) / GBM * (a->cout / BN);
   const int64_t tiles_s = (M + 63) / 64 * (a->cout / BN);
-  return tiles < 384 && tiles_s >= kShortMin;
+  const int nsteps = a->kernel * a->kernel * (a->cin / BK);
+  return tiles < 384 && (tiles_s >= 384 || (tiles_s >= 256 && nsteps <= 48));
 }
 
 // K-split for this shape: 1 unless the grid would leave most CUs idle (the 8x8-latent convs)

@@ -29,14 +29,13 @@
 //    scale (CDNA guide T13 hazard).
 #include "frame_attn.hpp"
 
+// the product form: two 32-query sets per wave, two waves per SIMD (O in arch VGPRs, builtin MFMAs
+// only); SETS 3 / WAVES 4 (one wave per SIMD, O in AGPRs) measured 0.85 vs 0.81 ms
 #ifndef VP2P_K1_PP_SETS
-#define VP2P_K1_PP_SETS 3
+#define VP2P_K1_PP_SETS 2
 #endif
 #ifndef VP2P_K1_PP_WAVES
-#define VP2P_K1_PP_WAVES 4
-#endif
-#ifndef VP2P_K1_PP_POLY
-#define VP2P_K1_PP_POLY 0
+#define VP2P_K1_PP_WAVES 8
 #endif
 
 namespace vp2p {
@@ -69,25 +68,6 @@ __device__ __forceinline__ bf16x4 ldtr(const lchar* p) {
 //  * v_cvt -> PV MFMA reading the packed P: one whole block apart;
 //  * VALU write of P / O in the rare rescale -> MFMA: the s_nop 1 opening every block;
 //  * PV MFMA -> VALU read of O: o_fence() (two s_nop 7).
-// 2^x of a pair on the plain VALU pipe (packed f32): t = x + 1.5*2^23 holds n = round(x) in its low
-// bits, f = x - n in [-0.5, 0.5], 2^f by the degree-2 minimax polynomial (relative error 1.7e-3,
-// under the half-ulp 3.9e-3 of the bf16 the result is rounded to), and n added into the exponent
-// field.  x is clamped at -126 so the exponent cannot wrap (2^-126 underflows to 0 in the bf16 P
-// anyway whenever it matters: P is normalised by a row sum >= 1).
-__device__ __forceinline__ f32x2 pexp2(f32x2 x) {
-  x[0] = fmaxf(x[0], -126.f);
-  x[1] = fmaxf(x[1], -126.f);
-  const f32x2 M = {12582912.f, 12582912.f};
-  const f32x2 t = x + M;
-  const f32x2 f = x - (t - M);
-  const f32x2 p = (f * f32x2{0.23842894f, 0.23842894f} + f32x2{0.70344818f, 0.70344818f}) * f +
-                  f32x2{1.0004431f, 1.0004431f};
-  f32x2 y;
-  y[0] = __uint_as_float(__float_as_uint(p[0]) + (__float_as_uint(t[0]) << 23));
-  y[1] = __uint_as_float(__float_as_uint(p[1]) + (__float_as_uint(t[1]) << 23));
-  return y;
-}
-
 __device__ __forceinline__ uint32_t vcvt(float x, float y) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x, y}, bf16x2));
 }
@@ -115,7 +95,7 @@ __device__ __forceinline__ void pv(f32x16& o, const bf16x8& v, const u32x4& p) {
 
 }  // namespace
 
-template <int SETS, int WAVES, int POLY>
+template <int SETS, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(const vp2p_frame_attn_args a) {
   static_assert(SETS >= 2, "the QK^T of the last set rides in group 0 of the next block");
   static_assert(WAVES == 4 || WAVES == 8, "one or two waves per SIMD");
@@ -286,17 +266,12 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(co
       uint32_t pn[8];
       f32x16 acc;
       const f32x16& sg = S[g];
-      // pair k = scores 2k, 2k+1: two v_exp, or (bit k of POLY) one packed polynomial on the plain
-      // VALU pipe, which leaves the transcendental unit to the other pairs
+      // pair k = scores 2k, 2k+1.  (Moving some pairs onto a packed-f32 polynomial 2^x to unload the
+      // transcendental unit measured slower, 0.92-1.02 vs 0.81 ms: the packed ops cost more issue
+      // than the v_exp they replace -- profiles/r04_issue_bench.jsonl, r04_k1_poly_ab.jsonl.)
       auto pair = [&](int k) {
-        if ((POLY >> k) & 1) {
-          const f32x2 y = pexp2(f32x2{sg[2 * k], sg[2 * k + 1]});
-          e[2 * k] = y[0];
-          e[2 * k + 1] = y[1];
-        } else {
-          e[2 * k] = fast_exp2(sg[2 * k]);
-          e[2 * k + 1] = fast_exp2(sg[2 * k + 1]);
-        }
+        e[2 * k] = fast_exp2(sg[2 * k]);
+        e[2 * k + 1] = fast_exp2(sg[2 * k + 1]);
       };
       // slot 0: pair 0 | QK k-step 0
       pair(0);
@@ -462,7 +437,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(co
 }
 
 int launch_frame_attn_pp(const vp2p_frame_attn_args* a, hipStream_t stream) {
-  constexpr int SETS = VP2P_K1_PP_SETS, WAVES = VP2P_K1_PP_WAVES, POLY = VP2P_K1_PP_POLY;
+  constexpr int SETS = VP2P_K1_PP_SETS, WAVES = VP2P_K1_PP_WAVES;
   if (a->dtype != VP2P_BF16 || a->head_dim != kD || !a->q_prescaled || a->tokens_kv % kKT) return VP2P_E_SHAPE;
   // 32-bit buffer offsets: every key row of one (b, head) within 4 GiB
   if ((int64_t)a->tokens_kv * a->k_sn * 2 >= (1ll << 32) || (int64_t)a->tokens_kv * a->v_sn * 2 >= (1ll << 32))
@@ -470,10 +445,10 @@ int launch_frame_attn_pp(const vp2p_frame_attn_args* a, hipStream_t stream) {
   const int FQ = a->frames * a->tokens_q;
   const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 32 * SETS * WAVES - 1) / (32 * SETS * WAVES));
   if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_pp<SETS, WAVES, POLY>),
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&frame_attn_kernel_pp<SETS, WAVES>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  hipLaunchKernelGGL((frame_attn_kernel_pp<SETS, WAVES, POLY>), dim3((unsigned)nwg), dim3(64 * WAVES), kLdsBytes, stream, *a);
+  hipLaunchKernelGGL((frame_attn_kernel_pp<SETS, WAVES>), dim3((unsigned)nwg), dim3(64 * WAVES), kLdsBytes, stream, *a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
