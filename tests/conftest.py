@@ -10,6 +10,8 @@ for p in (ROOT, os.path.join(ROOT, "video-p2p_amd"), os.path.join(ROOT, "tests",
 
 
 def pytest_configure(config):
+    from vp2p.tuning import use_tuned_libraries
+    use_tuned_libraries()            # before the first convolution initialises MIOpen
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built HIP library")
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
