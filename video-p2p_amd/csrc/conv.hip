@@ -575,16 +575,22 @@ static int launch_g(const vp2p_conv_args& a, dim3 grid, int am, hipStream_t s) {
 // tiles to give every CU one.  (A wide tile on 32-channel K-steps in a four-stage ring, three steps'
 // DMA in flight, measured bit-equal but 4-10 % slower on every shape:
 // profiles/r03_k10_deep_rejected.jsonl.)
-// auto: the wide tile wherever it gives every CU a tile (measured, profiles/r03_k10_wide_ab.jsonl,
-// bit-equal: 3x3 convs at 64^2 / 32^2 -6..-13 %, 1x1 GEMMs M 131072 K 320 / 1280 N 320 -5 / -21 %,
-// M 32768 K 640 N 640 -10 %; slower where it leaves CUs idle: 128-tile grids +3..+50 %)
-static bool wide_auto(const vp2p_conv_args* a) { return a->kernel == 3 || a->kernel == 1; }
+// The wide tile wherever it gives every CU a tile (measured, profiles/r03_k10_wide_ab.jsonl, bit-equal:
+// 3x3 convs at 64^2 / 32^2 -6..-13 %, 1x1 GEMMs M 131072 K 320 / 1280 N 320 -5 / -21 %, M 32768 K 640
+// N 640 -10 %; slower where it leaves CUs idle: 128-tile grids +3..+50 %) -- unless its grid ends in a
+// part-filled wave that the 128 x 160 grid (two workgroups per CU) does not: the wide tile's ~12 %
+// per-tile advantage against the two grids' last-wave fill (M 8192 K 1280 N 3840: 384 wide tiles =
+// 1.5 waves, 1536 128-row tiles = 3 full waves).
+static double wave_fill(int64_t tiles, int64_t slots) {
+  return (double)tiles / (double)(((tiles + slots - 1) / slots) * slots);
+}
 
 static int pick_tile(const vp2p_conv_args* a, int64_t M) {
   const int64_t tiles_b = (M + 255) / 256 * (a->cout / BN);
+  const int64_t tiles_0 = (M + GBM - 1) / GBM * (a->cout / BN);
   const bool wide_ok = a->cout % 320 == 0;    // plain and GEGLU epilogues (GEGLU: profiles/r03_k10_geglu_wide_ab.jsonl)
   const int64_t tiles_w = (M + 255) / 256 * (a->cout / 320);
-  if (wide_ok && tiles_w >= 256 && wide_auto(a)) return 2;
+  if (wide_ok && tiles_w >= 256 && 1.12 * wave_fill(tiles_w, 256) >= wave_fill(tiles_0, 512)) return 2;
   return (tiles_b >= 256 && a->kernel == 1 && a->cin >= 1280) ? 1 : 0;
 }
 

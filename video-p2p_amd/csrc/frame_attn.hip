@@ -566,12 +566,14 @@ static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
     constexpr int KT = D <= 64 ? 256 : 64;
     const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
     if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
+#ifndef VP2P_K1_LAB_X2F   // (lab builds only: x2f for every d = 40 launch, the A/B baseline)
     if constexpr (D == 40) {
       // the software-pipelined res-64 kernel (frame_attn_pp.hip) wherever its layout applies
       // (VP2P_E_SHAPE: it does not, x2f below takes the call)
       const int rc = launch_frame_attn_pp(a, stream);
       if (rc != VP2P_E_SHAPE) return rc;
     }
+#endif
     if constexpr (C::DP > D)
       if (a->q_prescaled) return launch_x2f<D, 128, true>(a, nwg, stream);
     return launch_x2f<D, KT, false>(a, nwg, stream);
