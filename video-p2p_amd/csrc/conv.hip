@@ -46,7 +46,6 @@ namespace vp2p {
 namespace conv {
 
 constexpr int BN = 160, BK = 64;
-constexpr int WTM = 4, WTN = 5;                 // 16x16 MFMA tiles per wave (64 x 80)
 constexpr int CROW = BN + 8;                    // epilogue tile row (elements)
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -79,8 +78,9 @@ constexpr int GBM = 128, NW = 4;                               // the split-K / 
 //     grid would leave CUs idle (1-2 frame edits), one pass where 0 needed a split-K second pass;
 // All: the same per-output K order and MFMA sequence (one 16x16x32 MFMA per 32 channels), so
 // bit-equal results.
-template <int TBM_, int TBN_, int WTM_, int NST_, int KB_ = 64> struct GTile {
-  static constexpr int TBM = TBM_, TBN = TBN_, WTM = WTM_, NSTAGE = NST_;
+template <int TBM_, int TBN_, int WTM_, int NST_, int KB_ = 64, int WTN_ = 5> struct GTile {
+  static constexpr int TBM = TBM_, TBN = TBN_, WTM = WTM_, WTN = WTN_, NSTAGE = NST_;
+  static constexpr int WN = 16 * WTN;                             // output columns per wave
   static constexpr int KB = KB_;                                  // channels per K-step
   static constexpr int RB = KB * 2;                               // LDS row bytes
   static constexpr int CPW = KB / 8;                              // 16-byte chunks per row
@@ -90,7 +90,7 @@ template <int TBM_, int TBN_, int WTM_, int NST_, int KB_ = 64> struct GTile {
     else return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);
   }
   static constexpr int WR = 16 * WTM;                             // output rows per wave
-  static constexpr int WCOL = TBN / 80;                           // waves along N (80 columns each)
+  static constexpr int WCOL = TBN / WN;                           // waves along N
   static constexpr int NWV = (TBM / WR) * WCOL;                   // waves
   static constexpr int NT = 64 * NWV;                             // threads
   static constexpr int STAGE = (TBM + TBN) * RB;                  // bytes per LDS stage (A then B)
@@ -106,6 +106,15 @@ template <> struct GCfg<0> : GTile<128, 160, 4, 2> {};
 template <> struct GCfg<1> : GTile<256, 160, 4, 3> {};
 template <> struct GCfg<2> : GTile<256, 320, 8, 2> {};
 template <> struct GCfg<3> : GTile<64, 160, 2, 2> {};
+// The GEGLU epilogue's form of each tile: the same block, threads, stages and LDS, with every wave
+// 160 columns wide (10 16-column tiles = 5 (value, gate) pairs of the same 16 channels: the weights
+// come interleaved per 16 as [16 value rows | 16 gate rows]), so a lane holds a channel's value and
+// gate for the same four rows itself -- no cross-lane exchange.
+template <int CF> struct GCfgG;
+template <> struct GCfgG<0> : GTile<128, 160, 2, 2, 64, 10> {};
+template <> struct GCfgG<1> : GTile<256, 160, 2, 3, 64, 10> {};
+template <> struct GCfgG<2> : GTile<256, 320, 4, 2, 64, 10> {};
+template <> struct GCfgG<3> : GTile<64, 160, 1, 2, 64, 10> {};
 constexpr int G_STAGE = GCfg<0>::STAGE;
 constexpr int G_LDS = GCfg<0>::LDS;
 
@@ -142,6 +151,37 @@ __device__ __forceinline__ f32x2v erf_fast2(f32x2v x) {
   return __builtin_elementwise_copysign((f32x2v)(1.f) - r, x);
 }
 
+typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
+// both lanes of a pair rounded to bf16 (round to nearest even) and back: one v_cvt_pk_bf16_f32, the
+// two halves unpacked by a shift and a mask
+__device__ __forceinline__ f32x2v round_bf16x2(f32x2v x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf16x2v));
+  return f32x2v{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
+
+__device__ __forceinline__ f32x4v round_bf16x4(f32x4v x) {
+  const f32x2v lo = round_bf16x2(f32x2v{x[0], x[1]}), hi = round_bf16x2(f32x2v{x[2], x[3]});
+  return f32x4v{lo[0], lo[1], hi[0], hi[1]};
+}
+
+// erf_fast2 on four values (two independent packed chains)
+__device__ __forceinline__ f32x4v erf_fast4(f32x4v x) {
+  const f32x4v ax = __builtin_elementwise_abs(x);
+  f32x4v p = __builtin_elementwise_fma(ax, (f32x4v)(4.30638e-5f), (f32x4v)(2.765672e-4f));
+  p = __builtin_elementwise_fma(p, ax, (f32x4v)(1.520143e-4f));
+  p = __builtin_elementwise_fma(p, ax, (f32x4v)(9.2705272e-3f));
+  p = __builtin_elementwise_fma(p, ax, (f32x4v)(4.22820123e-2f));
+  p = __builtin_elementwise_fma(p, ax, (f32x4v)(7.05230784e-2f));
+  p = __builtin_elementwise_fma(p, ax, (f32x4v)(1.f));
+  p *= p;
+  p *= p;
+  p *= p;
+  p *= p;
+  const f32x4v r = {__builtin_amdgcn_rcpf(p[0]), __builtin_amdgcn_rcpf(p[1]), __builtin_amdgcn_rcpf(p[2]),
+                    __builtin_amdgcn_rcpf(p[3])};
+  return __builtin_elementwise_copysign((f32x4v)(1.f) - r, x);
+}
+
 __device__ __forceinline__ float erf_fast(float x) {
   const float ax = fabsf(x);
   float p = __builtin_fmaf(ax, 4.30638e-5f, 2.765672e-4f);
@@ -168,7 +208,8 @@ __device__ __forceinline__ float erf_fast(float x) {
 // rebuilt per step (inputs beyond 2^31 bytes).
 template <int KS, int EPI, int AM, int CF>
 __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
-  using Cfg = GCfg<CF>;
+  using Cfg = std::conditional_t<EPI == 1, GCfgG<CF>, GCfg<CF>>;
+  static_assert(Cfg::NWV == GCfg<CF>::NWV && Cfg::LDS <= GCfg<CF>::LDS, "the launch's block and LDS");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w / Cfg::WCOL, wn = w - (w / Cfg::WCOL) * Cfg::WCOL;
@@ -320,11 +361,11 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     }
   };
 
-  f32x4v acc[Cfg::WTM][WTN];
+  f32x4v acc[Cfg::WTM][Cfg::WTN];
 #pragma unroll
   for (int i = 0; i < Cfg::WTM; ++i)
 #pragma unroll
-    for (int j = 0; j < WTN; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < Cfg::WTN; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
   const int fr = l & 15, fq = l >> 4;           // fragment row / 16-byte chunk within the 32-wide k-step
   // prologue: the first NSTAGE - 1 steps' DMA in flight (one step for the two-stage tiles)
@@ -369,21 +410,21 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     cur = cur + 1 == Cfg::NSTAGE ? 0 : cur + 1;
 #pragma unroll
     for (int ks = 0; ks < Cfg::CPW; ks += 4) {   // chunk index of the 32-channel MFMA k-step (0 or 4)
-      bf16x8 af[Cfg::WTM], bfr[WTN];
+      bf16x8 af[Cfg::WTM], bfr[Cfg::WTN];
 #pragma unroll
       for (int i = 0; i < Cfg::WTM; ++i) {
         const int r = wm * Cfg::WR + 16 * i + fr;
         af[i] = *reinterpret_cast<const bf16x8*>(As + r * Cfg::RB + Cfg::swz(r, ks + fq) * 16);
       }
 #pragma unroll
-      for (int j = 0; j < WTN; ++j) {
-        const int r = wn * 80 + 16 * j + fr;
+      for (int j = 0; j < Cfg::WTN; ++j) {
+        const int r = wn * Cfg::WN + 16 * j + fr;
         bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * Cfg::RB + Cfg::swz(r, ks + fq) * 16);
       }
 #pragma unroll
       for (int i = 0; i < Cfg::WTM; ++i)
 #pragma unroll
-        for (int j = 0; j < WTN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < Cfg::WTN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
   }
 
@@ -397,46 +438,54 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
         const int p = m0 + wm * Cfg::WR + 16 * i + 4 * fq + e;
         if (p < M) {
 #pragma unroll
-          for (int j = 0; j < WTN; ++j) ws[(int64_t)p * a.cout + n0 + wn * 80 + 16 * j + fr] = acc[i][j][e];
+          for (int j = 0; j < Cfg::WTN; ++j) ws[(int64_t)p * a.cout + n0 + wn * Cfg::WN + 16 * j + fr] = acc[i][j][e];
         }
       }
     return;
   }
   const bf16* bias = static_cast<const bf16*>(a.bias);
   if constexpr (EPI == 1) {
-    // GEGLU straight from the accumulators (no LDS staging): the weight rows are interleaved per 16
-    // as [8 value | 8 gate], so lane l (tile column l & 15 < 8) holds a channel's values and lane
-    // l ^ 8 its gates, for the same four rows 4 * fq + e.  One DPP exchange (row_ror:8) per pair of
-    // rows gives lane l (value, gate) of rows e = 0, 1 and lane l ^ 8 those of rows e = 2, 3; each
-    // lane then forms two outputs -- the projection rounded to bf16, gelu rounded, the product rounded,
-    // exactly K9's order -- on packed FP32.
+    // GEGLU straight from the accumulators: tile 2q of the wave holds the values and tile 2q + 1 the
+    // gates of the same 16 channels (weights interleaved per 16), so lane l has a channel's value and
+    // gate for rows 4 * fq + e, e = 0..3, and forms those four outputs on packed FP32 -- the
+    // projection rounded to bf16, gelu rounded, the product rounded, exactly K9's order.  The
+    // (TBM, TBN / 2) output tile is staged in LDS (free after the last K-step) and leaves as whole
+    // 16-byte row segments.
 #pragma clang fp contract(off)
     constexpr float kAlpha = 0.70710678118654752440f;
+    constexpr int OW = Cfg::TBN / 2, OROW = OW + 8;                 // output tile row (elements)
+    static_assert(Cfg::TBM * OROW * 2 <= Cfg::LDS, "GEGLU output tile in LDS");
     const int half = a.cout / 2;
-    bf16* y = static_cast<bf16*>(a.y);
-    const bool isv = fr < 8;
+    bf16* Os = reinterpret_cast<bf16*>(smem);
+    __syncthreads();                                                // every wave done with the stages
 #pragma unroll
-    for (int j = 0; j < WTN; ++j) {
-      const int gcol = n0 + wn * 80 + 16 * j + fr;            // interleaved projection column
-      const float bv = bias ? (float)bias[gcol] : 0.f;
-      const int oc = (gcol >> 4) * 8 + (fr & 7);              // output channel
+    for (int q = 0; q < Cfg::WTN / 2; ++q) {
+      const int gv = n0 + wn * Cfg::WN + 32 * q + fr;               // value column; gate: gv + 16
+      const float bv = bias ? (float)bias[gv] : 0.f, bg = bias ? (float)bias[gv + 16] : 0.f;
+      const int oc = wn * (Cfg::WN / 2) + 16 * q + fr;              // output channel within the tile
 #pragma unroll
       for (int i = 0; i < Cfg::WTM; ++i) {
-        float h[4];
+        const int rb = wm * Cfg::WR + 16 * i + 4 * fq;
+        {
+          // the lane's four rows as one 4-vector: every step is two independent packed ops, so the
+          // dependent-issue wait of packed FP32 never stalls
+          const f32x4v val = round_bf16x4(acc[i][2 * q] + bv);
+          const f32x4v g = round_bf16x4(acc[i][2 * q + 1] + bg);
+          const f32x4v ge = round_bf16x4(g * 0.5f * (1.f + erf_fast4(g * kAlpha)));
+          const f32x4v o = val * ge;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) h[e] = (float)(bf16)(acc[i][j][e] + bv);
-        const float sx = isv ? h[2] : h[0], sy = isv ? h[3] : h[1];
-        const float rx = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sx), 0x128, 0xf, 0xf, false));
-        const float ry = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sy), 0x128, 0xf, 0xf, false));
-        const f32x2v val = isv ? f32x2v{h[0], h[1]} : f32x2v{rx, ry};
-        const f32x2v g = isv ? f32x2v{rx, ry} : f32x2v{h[2], h[3]};
-        const f32x2v gl = g * 0.5f * (1.f + erf_fast2(g * kAlpha));
-        const f32x2v ge = {(float)(bf16)gl.x, (float)(bf16)gl.y};
-        const f32x2v o = val * ge;
-        const int p0 = m0 + wm * Cfg::WR + 16 * i + 4 * fq + (isv ? 0 : 2);
-        if (p0 < M) y[(int64_t)p0 * half + oc] = (bf16)o.x;
-        if (p0 + 1 < M) y[(int64_t)(p0 + 1) * half + oc] = (bf16)o.y;
+          for (int e = 0; e < 4; ++e) Os[(rb + e) * OROW + oc] = (bf16)o[e];
+        }
       }
+    }
+    __syncthreads();
+    bf16* y = static_cast<bf16*>(a.y);
+    for (int c = tid; c < Cfg::TBM * (OW / 8); c += Cfg::NT) {
+      const int row = c / (OW / 8), ch = c - row * (OW / 8);
+      const int p = m0 + row;
+      if (p < M)
+        *reinterpret_cast<bf16x8*>(y + (int64_t)p * half + n0 / 2 + ch * 8) =
+            *reinterpret_cast<const bf16x8*>(Os + row * OROW + ch * 8);
     }
     return;
   }
@@ -450,8 +499,8 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   if (wm * Cfg::WR / Cfg::EROWS == pass) {
     const int rb = wm * Cfg::WR - pass * Cfg::EROWS;
 #pragma unroll
-    for (int j = 0; j < WTN; ++j) {
-      const int col = wn * 80 + 16 * j + fr;
+    for (int j = 0; j < Cfg::WTN; ++j) {
+      const int col = wn * Cfg::WN + 16 * j + fr;
       const float bv = bias ? (float)bias[n0 + col] : 0.f;
 #pragma unroll
       for (int i = 0; i < Cfg::WTM; ++i)

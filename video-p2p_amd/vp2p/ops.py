@@ -748,16 +748,16 @@ CONV = ConvSelector()
 
 
 def geglu_interleave(weight: torch.Tensor, bias: Optional[torch.Tensor]):
-    """Row order K10's GEGLU epilogue expects: per 16 rows, 8 value rows then the 8 matching gate rows
-    (GEGLU.proj is [value; gate], diffusers' ``chunk(2, dim=-1)``), so that the two halves of every
-    16-column MFMA output tile hold a channel's value and gate in lanes l and l ^ 8."""
+    """Row order K10's GEGLU epilogue expects: per 32 rows, 16 value rows then the 16 matching gate
+    rows (GEGLU.proj is [value; gate], diffusers' ``chunk(2, dim=-1)``), so that a wave's MFMA output
+    tiles 2q and 2q + 1 hold the value and the gate of the same 16 channels in the same lanes."""
     n2, k = weight.shape
     inner = n2 // 2
     if inner % 80:
         raise ValueError("GEGLU inner width must be a multiple of 80")
-    t = inner // 8
-    w = torch.stack([weight[:inner].reshape(t, 8, k), weight[inner:].reshape(t, 8, k)], 1).reshape(n2, k)
-    b = None if bias is None else torch.stack([bias[:inner].reshape(t, 8), bias[inner:].reshape(t, 8)], 1).reshape(n2)
+    t = inner // 16
+    w = torch.stack([weight[:inner].reshape(t, 16, k), weight[inner:].reshape(t, 16, k)], 1).reshape(n2, k)
+    b = None if bias is None else torch.stack([bias[:inner].reshape(t, 16), bias[inner:].reshape(t, 16)], 1).reshape(n2)
     return w.contiguous(), (None if b is None else b.contiguous())
 
 
