@@ -503,10 +503,17 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       const int col = wn * Cfg::WN + 16 * j + fr;
       const float bv = bias ? (float)bias[n0 + col] : 0.f;
 #pragma unroll
-      for (int i = 0; i < Cfg::WTM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          Cs[(rb + 16 * i + 4 * fq + e) * Cfg::CROWV + col] = (bf16)((acc[i][j][e] + bv) * al);
+      for (int i = 0; i < Cfg::WTM; ++i) {
+        // the lane's four rows of the column as a 4-vector: packed adds / multiplies / conversions
+        const f32x4v v = (acc[i][j] + bv) * al;
+        const bf16x2v lo = __builtin_convertvector(f32x2v{v[0], v[1]}, bf16x2v);
+        const bf16x2v hi = __builtin_convertvector(f32x2v{v[2], v[3]}, bf16x2v);
+        bf16* c = Cs + (rb + 16 * i + 4 * fq) * Cfg::CROWV + col;
+        c[0] = lo.x;
+        c[Cfg::CROWV] = lo.y;
+        c[2 * Cfg::CROWV] = hi.x;
+        c[3 * Cfg::CROWV] = hi.y;
+      }
     }
   }
   __syncthreads();
