@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 14
+#define VP2P_ABI_VERSION 15
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -284,6 +284,14 @@ int vp2p_group_norm_apply_stats(const vp2p_group_norm_args* args, const float* s
  * B*parts*G*12 of the raw partials) -- and, after the gather, finalize nsets such triple arrays laid
  * out back to back into {mean, rstd} (batch, groups, 2) for vp2p_group_norm_apply_stats. */
 int vp2p_group_norm_merge(const vp2p_group_norm_args* args, const float* partials, float* triples, void* stream);
+/* The same two merges over a partial array of `parts` entries per (batch, group) produced elsewhere
+ * (vp2p_conv_args.gn_partials: the producing convolution's epilogue) instead of by _stats:
+ * _finalize_parts -> {mean, rstd} (batch, groups, 2) for vp2p_group_norm_apply_stats, _merge_parts ->
+ * the (batch, groups, 3) triples of a frame-sharded exchange. */
+int vp2p_group_norm_finalize_parts(const vp2p_group_norm_args* args, const float* partials, int32_t parts,
+                                   float* stats, void* stream);
+int vp2p_group_norm_merge_parts(const vp2p_group_norm_args* args, const float* partials, int32_t parts,
+                                float* triples, void* stream);
 int vp2p_group_norm_finalize_merged(const vp2p_group_norm_args* args, const float* triples, int32_t nsets,
                                     float* stats, void* stream);
 
@@ -361,9 +369,25 @@ typedef struct vp2p_conv_args {
    * max, torch.addmm(bias, x, w^T, beta=alpha, alpha=alpha) of the reference-precision path);
    * 0 = 1 (zero-initialised callers). */
   float alpha;
+  /* (since ABI 15) a per-image add after the bias -- the resnet's h + temb (resnet.py:149-156):
+   * y = round(round(x * w + bias) + img_add[p / (out_h * out_w), c]), img_add (batch, cout) dtype, the
+   * two roundings of the reference; NULL = none.  Plain one-pass epilogue without a residual. */
+  const void* img_add;
+  /* (since ABI 15) GroupNorm statistics of the stored output (the next norm2, resnet.py:158), written
+   * by the epilogue: (count, mean, M2) fp32 per (statistics sample s, M tile t, group g) at
+   * gn_partials[((s * parts + t) * gn_groups + g) * 3], s = p / gn_rows, parts =
+   * vp2p_conv2d_gn_parts(); NULL = none.  gn_rows: output pixels per sample (frames * out_h * out_w). */
+  float* gn_partials;
+  int32_t gn_groups;
+  int32_t gn_rows;
 } vp2p_conv_args;
 
 int vp2p_conv2d_supported(const vp2p_conv_args* args);
+/* M tiles per GroupNorm statistics sample of the tile this launch would use (the partial count per
+ * (sample, group) that gn_partials receives), or <= 0 when the shape cannot produce them in the
+ * epilogue (split-K, a residual / GEGLU / scaled epilogue, gn_rows not a multiple of the tile, groups
+ * not whole within a tile). */
+int32_t vp2p_conv2d_gn_parts(const vp2p_conv_args* args);
 /* Workspace the shape wants for split-K (small-M shapes: fewer tiles than CUs); 0 = none. */
 int64_t vp2p_conv2d_workspace_bytes(const vp2p_conv_args* args);
 int vp2p_conv2d_fwd(const vp2p_conv_args* args, void* stream);

@@ -233,3 +233,35 @@ def test_attn_temp_residual_on_output_projection(mode):
     assert err < 1e-2, err
     if mode == "library":
         assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("n,frames,c,h,cout,groups", [(8, 4, 320, 64, 320, 32), (8, 8, 640, 32, 640, 32),
+                                                      (16, 8, 320, 32, 640, 32), (4, 2, 640, 64, 320, 32)])
+def test_conv2d_gn_stats(n, frames, c, h, cout, groups):
+    """conv1 + temb with norm2's statistics left by K10's epilogue (ops.conv2d_gn): the output equals
+    the separate conv + add bit for bit (same tile, same two roundings), and the GroupNorm applied
+    from the epilogue's partials matches the GroupNorm with its own statistics pass."""
+    from vp2p import ops
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(n, c, h, h, generator=g).to(torch.bfloat16).to(DEV).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(cout, c, 3, 3, generator=g) / (c * 9) ** 0.5).to(torch.bfloat16).to(DEV)
+    w = w.contiguous(memory_format=torch.channels_last)
+    b = (torch.randn(cout, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    t = (torch.randn(n, cout, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    gw = (1 + 0.1 * torch.randn(cout, generator=g)).to(torch.bfloat16).to(DEV)
+    gb = (0.1 * torch.randn(cout, generator=g)).to(torch.bfloat16).to(DEV)
+    with torch.no_grad():
+        r = ops.conv2d_gn(x, w, b, 1, 1, t, groups, frames)
+        assert r is not None, "fused statistics unsupported for this shape"
+        y, stats = r
+        ref = (ops.conv2d(x, w, b, 1, 1).float() + t.float()[:, :, None, None]).to(torch.bfloat16)
+        assert torch.equal(y, ref)
+        got = ops.group_norm_from_partials(y, groups, gw, gb, 1e-5, frames, stats, silu=True)
+        want = ops.group_norm(ref.contiguous(memory_format=torch.channels_last), groups, gw, gb, 1e-5, frames, silu=True)
+        f32 = torch.nn.functional.group_norm(ref.float().reshape(n // frames, frames, cout, h, h).transpose(1, 2),
+                                             groups, gw.float(), gb.float(), 1e-5)
+        f32 = torch.nn.functional.silu(f32.transpose(1, 2).reshape(n, cout, h, h))
+    torch.cuda.synchronize()
+    err = (got.float() - f32).abs().max().item() / f32.abs().max().item()
+    assert err < 1e-2, err
+    assert (got.float() - want.float()).abs().max().item() <= 2 * (want.float() - f32).abs().max().item() + 1e-3

@@ -119,6 +119,19 @@ constexpr int G_STAGE = GCfg<0>::STAGE;
 constexpr int G_LDS = GCfg<0>::LDS;
 
 
+struct Welford {
+  float n, mean, m2;
+};
+// Chan's merge of two (count, mean, M2) summaries (the K7 GroupNorm partial format, norm.hip)
+__device__ __forceinline__ Welford wmerge(Welford a, Welford b) {
+  const float n = a.n + b.n;
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float d = b.mean - a.mean;
+  const float fb = b.n / n;
+  return {n, a.mean + d * fb, a.m2 + b.m2 + d * d * a.n * fb};
+}
+
 // LDS-DMA destination (a non-template helper: the address-space cast of a TBM-dependent expression
 // inside the kernel template makes hipcc's host pass silently drop the kernel's launch stub)
 __device__ __forceinline__ __attribute__((address_space(3))) void* to_lds(const char* p) {
@@ -492,7 +505,19 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   bf16* Cs = reinterpret_cast<bf16*>(smem);
   const float al = a.alpha == 0.f ? 1.f : a.alpha;     // x 1.0f is exact: alpha-free callers unchanged
   const bf16* res = static_cast<const bf16*>(a.residual);
+  const bf16* iadd = static_cast<const bf16*>(a.img_add);
+  const int hw = a.out_h * a.out_w;
   bf16* y = static_cast<bf16*>(a.y);
+  // GroupNorm statistics of the stored tile (vp2p_conv2d_gn_parts checked the geometry): the tile
+  // holds GT whole groups of cg channels; tpg threads per group, each summing fixed channel pairs over
+  // a stride of rows (shifted sums, the shift its first value), merged (Chan) across the tpg lanes
+  const bool gn = a.gn_partials != nullptr;
+  const int cg = gn ? a.cout / a.gn_groups : 2, GT = Cfg::TBN / cg, tpg = Cfg::NT / GT, hc = cg >> 1;
+  const int gi = tid / tpg, gk = tid - gi * tpg, grs = tpg / hc;          // rows per step
+  const bool gact = gk < grs * hc;
+  const int gcp = gk % hc, gr0 = gk / hc;
+  float gK = 0.f, gs1 = 0.f, gs2 = 0.f;
+  int gn_n = 0;
   // rows [pass * EROWS, (pass + 1) * EROWS) of the tile go through the LDS tile at a time
   for (int pass = 0; pass < Cfg::TBM / Cfg::EROWS; ++pass) {
   __syncthreads();
@@ -529,8 +554,43 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)rv[j]);
     }
+    if (iadd) {        // h + temb: the image's vector, one more rounding (resnet.py:149-156)
+      const bf16x8 tv = *reinterpret_cast<const bf16x8*>(iadd + (int64_t)(p / hw) * a.cout + n0 + ch * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)tv[j]);
+    }
     *reinterpret_cast<bf16x8*>(y + o) = v;
+    if (gn) *reinterpret_cast<bf16x8*>(Cs + row * Cfg::CROWV + ch * 8) = v;   // the stored values
   }
+  if (gn) {
+    __syncthreads();
+    if (gact) {
+      for (int r = gr0; r < Cfg::EROWS; r += grs) {
+        const bf16x2v t = *reinterpret_cast<const bf16x2v*>(Cs + r * Cfg::CROWV + gi * cg + 2 * gcp);
+        const float x0 = (float)t.x, x1 = (float)t.y;
+        if (gn_n == 0) gK = x0;
+        const float d0 = x0 - gK, d1 = x1 - gK;
+        gs1 += d0 + d1;
+        gs2 = fmaf(d0, d0, fmaf(d1, d1, gs2));
+        gn_n += 2;
+      }
+    }
+  }
+  }
+  if (gn) {
+    const float fn = (float)gn_n, inv = gn_n ? 1.f / fn : 0.f;
+    Welford w = {fn, gK + gs1 * inv, fmaxf(gs2 - gs1 * gs1 * inv, 0.f)};
+    for (int off = tpg >> 1; off > 0; off >>= 1) {
+      const Welford o = {__shfl_xor(w.n, off), __shfl_xor(w.mean, off), __shfl_xor(w.m2, off)};
+      w = wmerge(w, o);
+    }
+    if (gk == 0) {
+      const int parts = a.gn_rows / Cfg::TBM, smp = m0 / a.gn_rows, t = (m0 - smp * a.gn_rows) / Cfg::TBM;
+      float* o = a.gn_partials + (((int64_t)smp * parts + t) * a.gn_groups + n0 / cg + gi) * 3;
+      o[0] = w.n;
+      o[1] = w.mean;
+      o[2] = w.m2;
+    }
   }
 }
 
@@ -588,12 +648,15 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(const vp2p_conv_args a
   }
   const bf16* bias = static_cast<const bf16*>(a.bias);
   const bf16* res = static_cast<const bf16*>(a.residual);
+  const bf16* iadd = static_cast<const bf16*>(a.img_add);
+  const int64_t hw = (int64_t)a.out_h * a.out_w;
   const float al = a.alpha == 0.f ? 1.f : a.alpha;
   bf16x8 out;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float t = (float)(bf16)((v[j] + (bias ? (float)bias[c0 + j] : 0.f)) * al);
     if (res) t = t + (float)res[o + j];
+    if (iadd) t = t + (float)iadd[(p / hw) * a.cout + c0 + j];
     out[j] = (bf16)t;
   }
   *reinterpret_cast<bf16x8*>(static_cast<bf16*>(a.y) + o) = out;
@@ -695,6 +758,7 @@ extern "C" int vp2p_conv2d_supported(const vp2p_conv_args* a) {
   if (a->alpha != 0.f && a->alpha != 1.f && (a->residual || a->epilogue != VP2P_CONV_EPI_NONE)) return 0;
   if (!(a->alpha == a->alpha) || a->alpha > 3.0e38f || a->alpha < -3.0e38f) return 0;   // NaN / inf
   if (a->upsample != 0 && (a->upsample != 1 || a->stride != 1 || (a->in_h & 1) || (a->in_w & 1))) return 0;
+  if (a->img_add && (a->residual || a->epilogue != VP2P_CONV_EPI_NONE)) return 0;
   if (a->x2 || a->cin2) {   // two-source input: 1x1 convs on the buffer-offset form only
     if (!a->x2 || a->cin2 <= 0 || a->cin2 >= a->cin || a->cin2 % conv::BK || a->kernel != 1 || a->stride != 1 ||
         a->upsample || a->epilogue != VP2P_CONV_EPI_NONE)
@@ -702,6 +766,38 @@ extern "C" int vp2p_conv2d_supported(const vp2p_conv_args* a) {
     if ((int64_t)a->batch * a->in_h * a->in_w * a->cin * 2 >= ((int64_t)1 << 31)) return 0;
   }
   return 1;
+}
+
+namespace vp2p {
+namespace conv {
+// (TBM, TBN, threads) of the one-pass tile vp2p_conv2d_fwd picks for this shape (CF as in the launch)
+static void one_pass_tile(const vp2p_conv_args* a, int64_t M, int* tbm, int* tbn, int* nt) {
+  int cf = short_tile(a, M) ? 3 : pick_tile(a, M);
+  switch (cf) {
+    case 1: *tbm = GCfg<1>::TBM; *tbn = GCfg<1>::TBN; *nt = GCfg<1>::NT; break;
+    case 2: *tbm = GCfg<2>::TBM; *tbn = GCfg<2>::TBN; *nt = GCfg<2>::NT; break;
+    case 3: *tbm = GCfg<3>::TBM; *tbn = GCfg<3>::TBN; *nt = GCfg<3>::NT; break;
+    default: *tbm = GCfg<0>::TBM; *tbn = GCfg<0>::TBN; *nt = GCfg<0>::NT; break;
+  }
+}
+}  // namespace conv
+}  // namespace vp2p
+
+extern "C" int32_t vp2p_conv2d_gn_parts(const vp2p_conv_args* a) {
+  if (!a || !vp2p_conv2d_supported(a)) return 0;
+  if (a->epilogue != VP2P_CONV_EPI_NONE || a->residual || (a->alpha != 0.f && a->alpha != 1.f)) return 0;
+  if (conv::pick_ksplit(a) > 1) return 0;                       // statistics in the one-pass epilogue only
+  const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
+  if (a->gn_groups <= 0 || a->cout % a->gn_groups || a->gn_rows <= 0 || M % a->gn_rows) return 0;
+  const int cg = a->cout / a->gn_groups;
+  int tbm, tbn, nt;
+  conv::one_pass_tile(a, M, &tbm, &tbn, &nt);
+  if (cg % 2 || tbn % cg || a->gn_rows % tbm) return 0;
+  const int gt = tbn / cg;
+  if (nt % gt) return 0;
+  const int tpg = nt / gt;
+  if (tpg > 64 || (tpg & (tpg - 1)) || tpg < cg / 2) return 0;   // one wave per group, >= one row of pairs
+  return a->gn_rows / tbm;
 }
 
 extern "C" int64_t vp2p_conv2d_workspace_bytes(const vp2p_conv_args* a) {
@@ -715,8 +811,9 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   if (a->dtype != VP2P_BF16) return VP2P_E_DTYPE;
   if (!vp2p_conv2d_supported(a)) return VP2P_E_SHAPE;
   for (const void* p : {a->x, a->w, static_cast<const void*>(a->y), a->residual,
-                        static_cast<const void*>(a->workspace), a->x2})
+                        static_cast<const void*>(a->workspace), a->x2, a->img_add})
     if (reinterpret_cast<uintptr_t>(p) & 15) return VP2P_E_ARG;
+  if (a->gn_partials && vp2p_conv2d_gn_parts(a) <= 0) return VP2P_E_SHAPE;
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   if (M * a->cout > ((int64_t)1 << 40)) return VP2P_E_SHAPE;
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -825,6 +825,30 @@ extern "C" int vp2p_group_norm_merge(const vp2p_group_norm_args* a, const float*
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
+extern "C" int vp2p_group_norm_finalize_parts(const vp2p_group_norm_args* a, const float* partials, int32_t parts,
+                                              float* stats, void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!partials || !stats || parts <= 0) return VP2P_E_ARG;
+  g.parts = parts;
+  hipLaunchKernelGGL(gn_finalize_kernel<false>, dim3(a->groups, a->batch), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), *a, g, partials, 1, stats);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_merge_parts(const vp2p_group_norm_args* a, const float* partials, int32_t parts,
+                                           float* triples, void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!partials || !triples || parts <= 0) return VP2P_E_ARG;
+  g.parts = parts;
+  hipLaunchKernelGGL(gn_finalize_kernel<true>, dim3(a->groups, a->batch), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), *a, g, partials, 1, triples);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
 extern "C" int vp2p_group_norm_finalize_merged(const vp2p_group_norm_args* a, const float* triples, int32_t nsets,
                                                float* stats, void* stream) {
   GnGeom g;

@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
@@ -29,7 +29,8 @@ EXPORTS = ("vp2p_frame_attn_fwd", "vp2p_cross_kv_workspace_bytes", "vp2p_cross_k
            "vp2p_group_norm_bwd_reduce", "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd",
            "vp2p_nulltext_loss", "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
            "vp2p_add_layer_norm_fwd", "vp2p_conv2d_workspace_bytes", "vp2p_group_norm_finalize",
-           "vp2p_group_norm_apply_stats", "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged")
+           "vp2p_group_norm_apply_stats", "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged",
+           "vp2p_group_norm_finalize_parts", "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts")
 
 
 class GroupNormArgs(ctypes.Structure):
@@ -45,7 +46,8 @@ class ConvArgs(ctypes.Structure):
                 ("cout", c_int32), ("out_h", c_int32), ("out_w", c_int32),
                 ("kernel", c_int32), ("stride", c_int32), ("pad", c_int32), ("dtype", c_int32),
                 ("epilogue", c_int32), ("workspace", c_void_p), ("ksplit", c_int32),
-                ("upsample", c_int32), ("x2", c_void_p), ("cin2", c_int32), ("alpha", c_float)]
+                ("upsample", c_int32), ("x2", c_void_p), ("cin2", c_int32), ("alpha", c_float),
+                ("img_add", c_void_p), ("gn_partials", c_void_p), ("gn_groups", c_int32), ("gn_rows", c_int32)]
 
 
 class LayerNormArgs(ctypes.Structure):
@@ -176,6 +178,9 @@ def load(path: str = None):
     lib.vp2p_conv2d_supported.argtypes = [POINTER(ConvArgs)]
     lib.vp2p_conv2d_fwd.argtypes = [POINTER(ConvArgs), c_void_p]
     lib.vp2p_conv2d_workspace_bytes.argtypes = [POINTER(ConvArgs)]
+    lib.vp2p_conv2d_gn_parts.argtypes = [POINTER(ConvArgs)]
+    lib.vp2p_group_norm_finalize_parts.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p]
+    lib.vp2p_group_norm_merge_parts.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p]
     lib.vp2p_conv2d_workspace_bytes.restype = c_int64
     lib.vp2p_add_layer_norm_fwd.argtypes = [POINTER(LayerNormArgs), c_void_p, c_void_p, c_void_p]
     for name in ("vp2p_frame_attn_fwd", "vp2p_cross_kv_prep", "vp2p_cross_attn_p2p_fwd",
@@ -186,7 +191,8 @@ def load(path: str = None):
                  "vp2p_group_norm_bwd_apply", "vp2p_layer_norm_bwd", "vp2p_geglu_bwd", "vp2p_nulltext_loss",
                  "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
                  "vp2p_add_layer_norm_fwd", "vp2p_group_norm_finalize", "vp2p_group_norm_apply_stats",
-                 "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged"):
+                 "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged", "vp2p_group_norm_finalize_parts",
+                 "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts"):
         getattr(lib, name).restype = c_int32
     if lib.vp2p_abi_version() != ABI_VERSION:
         raise Vp2pError(f"{p}: ABI version {lib.vp2p_abi_version()} != {ABI_VERSION}; rebuild")

@@ -664,6 +664,72 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
     return y
 
 
+_CONV_GN_PARTS = {}   # (conv geometry, groups, rows) -> statistics partials per sample (<= 0: none)
+
+
+def conv2d_gn(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
+              img_add: Optional[torch.Tensor], groups: int, frames: int):
+    """K10 ``conv(x) + img_add[image]`` (the resnet's ``conv1(.) + temb``, resnet.py:146-156: two
+    roundings) that also leaves the GroupNorm statistics of its output -- the next norm2's
+    (resnet.py:158), ``groups`` groups over ``frames`` consecutive images -- as per-tile (count, mean,
+    M2) partials written by the epilogue, so the GroupNorm needs no statistics pass.  Returns
+    (y, (partials, parts)), or None when the shape cannot produce them in one pass (split-K, tile /
+    group geometry): the caller then runs the conv and the GroupNorm as usual."""
+    if not x.is_contiguous(memory_format=torch.channels_last) or x.dtype != torch.bfloat16:
+        return None
+    w = weight if weight.is_contiguous(memory_format=torch.channels_last) else \
+        weight.contiguous(memory_format=torch.channels_last)
+    if bias is not None and (bias.dtype != x.dtype or not bias.is_contiguous()):
+        bias = bias.to(x.dtype).contiguous()
+    a, shape = _conv_args(x, w, bias, None, None, stride, padding)
+    N, Cout, Ho, Wo = shape
+    if N % frames or (img_add is not None and (tuple(img_add.shape) != (N, Cout) or img_add.dtype != x.dtype)):
+        return None
+    a.gn_groups, a.gn_rows = groups, frames * Ho * Wo
+    lib = _lib.load()
+    key = (a.batch, a.in_h, a.in_w, a.cin, a.cout, a.kernel, a.stride, a.pad, groups, frames)
+    parts = _CONV_GN_PARTS.get(key)
+    if parts is None:
+        parts = _CONV_GN_PARTS[key] = int(lib.vp2p_conv2d_gn_parts(ctypes.byref(a)))
+    if parts <= 0:
+        return None
+    y = torch.empty(shape, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    partials = torch.empty((N // frames) * parts * groups * 3, device=x.device, dtype=torch.float32)
+    if img_add is not None:
+        img_add = img_add.contiguous()
+        a.img_add = _ptr(img_add)
+    a.y, a.gn_partials = _ptr(y), _ptr(partials)
+    check(lib.vp2p_conv2d_fwd(ctypes.byref(a), _stream()), "vp2p_conv2d_fwd(gn)")
+    return y, (partials, parts)
+
+
+def group_norm_from_partials(x: torch.Tensor, num_groups: int, weight: Optional[torch.Tensor],
+                             bias: Optional[torch.Tensor], eps: float, frames: int, stats, silu: bool = False,
+                             shard=None) -> torch.Tensor:
+    """The apply half of ``group_norm`` on statistics its producer left (``conv2d_gn``): the
+    partials are merged into {mean, rstd} per (batch, group) -- across the frame shards' ranks
+    through the merged-triple exchange -- and one apply launch normalises (+ SiLU)."""
+    partials, parts = stats
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    a = _gn_args(x, num_groups, weight, bias, eps, frames, silu, None, out)
+    lib = _lib.load()
+    s = _stream()
+    B = x.shape[0] // frames
+    st = torch.empty(B * num_groups * 2, device=x.device, dtype=torch.float32)
+    if shard is not None and shard.world > 1:
+        tri = torch.empty(B * num_groups * 3, device=x.device, dtype=torch.float32)
+        check(lib.vp2p_group_norm_merge_parts(ctypes.byref(a), _ptr(partials), parts, _ptr(tri), s),
+              "vp2p_group_norm_merge_parts")
+        tri = shard.all_gather_flat(tri)
+        check(lib.vp2p_group_norm_finalize_merged(ctypes.byref(a), _ptr(tri), shard.world, _ptr(st), s),
+              "vp2p_group_norm_finalize_merged")
+    else:
+        check(lib.vp2p_group_norm_finalize_parts(ctypes.byref(a), _ptr(partials), parts, _ptr(st), s),
+              "vp2p_group_norm_finalize_parts")
+    check(lib.vp2p_group_norm_apply_stats(ctypes.byref(a), _ptr(st), s), "vp2p_group_norm_apply_stats")
+    return out
+
+
 class ConvSelector:
     """Per-shape choice between a K10 launch and the library path (MIOpen convolution, hipBLASLt
     GEMM + K9 / a separate add).
@@ -727,6 +793,18 @@ class ConvSelector:
         if self.pick(key, sup, k10, lib):
             return k10()
         return lib()
+
+    def prefers_k10(self, x, weight, stride: int, padding: int) -> bool:
+        """Whether ``run`` would take K10 for this plain convolution (no residual, upsample or second
+        source) -- without running anything ("tune" mode: no, it times on first use)."""
+        if self.mode == "tune":
+            return False
+        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, False, False)
+        skey = (key, False, x.dtype, weight.dtype, x.is_cuda, x.is_contiguous(memory_format=torch.channels_last), True)
+        sup = self._supported.get(skey)
+        if sup is None:
+            sup = self._supported[skey] = conv2d_supported(x, weight, stride, padding)
+        return self.pick(key, sup, None, None)
 
     @staticmethod
     def _faster(k10, library) -> bool:

@@ -185,15 +185,39 @@ class ResnetBlock3D(nn.Module):
         UpBlock3D), read by norm1 and conv_shortcut from the two tensors (the cat is never written)."""
         if skip is not None and self.conv_shortcut is None:
             x, skip = torch.cat([x, skip], dim=1), None
-        h = self.conv1(group_norm_frames(x, self.norm1, frames, silu=True, x2=skip))
+        hn = group_norm_frames(x, self.norm1, frames, silu=True, x2=skip)
         pre = self.__dict__.get("_temb_pre")      # this block's slice of UNet3D's batched projection
         t = pre if pre is not None else self.time_emb_proj(F.silu(temb))
-        t = t.repeat_interleave(frames, 0).to(h.dtype)
+        t = t.repeat_interleave(frames, 0).to(hn.dtype)
+        fused = None
+        if self._conv1_gn_ok(hn, t):
+            # conv1 + temb on K10 with norm2's statistics left by its epilogue: no statistics pass
+            fused = ops.conv2d_gn(hn, self.conv1.weight, self.conv1.bias, 1, 1, t, self.norm2.num_groups, frames)
         sc = x if self.conv_shortcut is None else self.conv_shortcut(x, x2=skip)
-        h = self.dropout(group_norm_frames(h, self.norm2, frames, silu=True, add=t))
+        if fused is not None:
+            h, stats = fused
+            n2 = self.norm2
+            h = ops.group_norm_from_partials(h, n2.num_groups, n2.weight, n2.bias, n2.eps, frames, stats, silu=True,
+                                             shard=frame_parallel.active() if frames > 1 else None)
+        else:
+            h = self.conv1(hn)
+            h = self.dropout(group_norm_frames(h, self.norm2, frames, silu=True, add=t))
         if self.output_scale_factor != 1.0:
             return (sc + self.conv2(h)) / self.output_scale_factor
         return self.conv2(h, residual=sc)          # sc + conv2(h): the add fused into K10's epilogue
+
+
+    def _conv1_gn_ok(self, hn, t) -> bool:
+        """The fused conv1 + temb + norm2-statistics path: inference, bf16 K10 (the per-shape table
+        picks K10 for conv1), a plain InflatedConv3d / GroupNorm pair, dropout inactive."""
+        c1, n2 = self.conv1, self.norm2
+        if autograd.needs_grad(hn, c1.weight, c1.bias, t, n2.weight, n2.bias) or (self.training and self.dropout.p):
+            return False
+        if type(c1) is not InflatedConv3d or c1._forward_hooks or c1._forward_pre_hooks or not n2.affine:
+            return False
+        if hn.dtype != torch.bfloat16 or not hn.is_cuda or c1.kernel_size != (3, 3) or c1.stride != (1, 1):
+            return False
+        return ops.CONV.prefers_k10(hn, c1.weight, 1, 1)
 
 
 class GEGLU(nn.Module):
