@@ -339,12 +339,18 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
         const uint32_t xs = (uint32_t)(((kh * a.in_w + kw) * cin1 + c0) * 2);
 #pragma unroll
         for (int i = 0; i < Cfg::ADMA; ++i)
+#if defined(VP2P_K10_DIAG) && (VP2P_K10_DIAG & 4)      // lab: no A DMA
+          if (false)
+#endif
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(As + Cfg::RPI * (w + Cfg::NWV * i) * Cfg::RB),
                                                    16, (a_off[i] + xs) | ((a_bad[i] >> tap) << 31), 0, 0, 0);
       }
       const uint32_t ws = (uint32_t)((tap * a.cin + c0) * 2);
 #pragma unroll
       for (int i = 0; i < Cfg::BDMA; ++i)
+#if defined(VP2P_K10_DIAG) && (VP2P_K10_DIAG & 8)      // lab: no B DMA
+        if (false)
+#endif
         if (Cfg::BDMA * Cfg::NWV == Cfg::BBLK || i < nbd)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, to_lds(Bs + Cfg::RPI * (w + Cfg::NWV * i) * Cfg::RB),
                                                    16, b_off[i] + ws, 0, 0, 0);
@@ -394,7 +400,7 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
 #ifndef VP2P_K10_DIAG
       __syncthreads();                            // vmcnt(0): step's DMA landed; step-1's reads done
       if (step + 1 < s_end) dma(step + 1, cur ^ 1);
-#else   // lab diagnostics only (wrong results): 1 = no main-loop DMA, 3 = no DMA and no barrier
+#else   // lab diagnostics only (wrong results): 1 = no main-loop DMA, 2 = no barrier, 4 / 8 = no A / B DMA
       if (!(VP2P_K10_DIAG & 2)) __syncthreads();
       if (!(VP2P_K10_DIAG & 1) && step + 1 < s_end) dma(step + 1, cur ^ 1);
 #endif
