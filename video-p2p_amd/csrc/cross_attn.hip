@@ -671,12 +671,20 @@ __global__ __launch_bounds__(512, 1) void cross_attn_kernel_v3e(const vp2p_cross
       *reinterpret_cast<u32x4*>(Vs + row * V3::VROW + c) = *reinterpret_cast<const u32x4*>(src + row * KP + c);
     }
   }
+  // the edit of run_videop2p.py:304-317 folded per word into new = G * A + P_edit * B: G the source
+  // term (Refine: P_src[mapper[w]]; Replace: sum_j P_src[j] M[j, w]; otherwise P_src[w]), A = a eq al,
+  // B = (1 - a) eq al + (1 - al) (Refine; a = 0 and the (1 - a) term dropped otherwise), al = alpha_t[w],
+  // eq the Reweight equalizer (1 without): one gather and one FMA per score instead of the chain
   for (int i = tid; i < NKV; i += 512) {
+    const bool refine = a.edit_mode == VP2P_EDIT_REFINE;
+    const float ra = refine ? a.refine_alpha[i] : 0.f;
+    const float eq = a.reweight ? a.equalizer[i] : 1.f;
+    const float al = a.alpha_words[i];
     f32x4 t;
-    t[0] = a.edit_mode == VP2P_EDIT_REFINE ? a.refine_alpha[i] : 0.f;
-    t[1] = a.reweight ? a.equalizer[i] : 1.f;
-    t[2] = a.alpha_words[i];
-    t[3] = __int_as_float(a.edit_mode == VP2P_EDIT_REFINE ? a.map_idx[i] : i);
+    t[0] = (refine ? ra : 1.f) * eq * al;
+    t[1] = (refine ? (1.f - ra) * eq * al : 0.f) + (1.f - al);
+    t[2] = 0.f;
+    t[3] = __int_as_float(refine ? a.map_idx[i] : i);
     etab[i] = t;
   }
   if (lb)
@@ -770,27 +778,21 @@ __global__ __launch_bounds__(512, 1) void cross_attn_kernel_v3e(const vp2p_cross
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       } else {
-#pragma clang fp contract(off)
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int wd = kb * 32 + acc_row(i, h);
             if (wd < NKV) {
-              const float pe_val = sc[kb][i];
               const f32x4 t = etab[wd];
-              float R;
+              float G;
               if (a.edit_mode == VP2P_EDIT_REPLACE) {
-                float gsum = 0.f;
-                for (int n = a.map_ptr[wd]; n < a.map_ptr[wd + 1]; ++n) gsum += psrc[a.map_idx[n]] * a.map_val[n];
-                R = gsum;
-              } else if (a.edit_mode == VP2P_EDIT_REFINE) {
-                R = psrc[__float_as_int(t[3])] * t[0] + pe_val * (1.f - t[0]);
+                G = 0.f;
+                for (int n = a.map_ptr[wd]; n < a.map_ptr[wd + 1]; ++n) G += psrc[a.map_idx[n]] * a.map_val[n];
               } else {
-                R = psrc[wd];
+                G = psrc[__float_as_int(t[3])];
               }
-              R = R * t[1];
-              sc[kb][i] = R * t[2] + (1.f - t[2]) * pe_val;
+              sc[kb][i] = __builtin_fmaf(G, t[0], sc[kb][i] * t[1]);
             }
           }
       }
