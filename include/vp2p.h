@@ -385,8 +385,8 @@ typedef struct vp2p_conv_args {
 int vp2p_conv2d_supported(const vp2p_conv_args* args);
 /* M tiles per GroupNorm statistics sample of the tile this launch would use (the partial count per
  * (sample, group) that gn_partials receives), or <= 0 when the shape cannot produce them in the
- * epilogue (split-K, a residual / GEGLU / scaled epilogue, gn_rows not a multiple of the tile, groups
- * not whole within a tile). */
+ * epilogue (split-K, a GEGLU / scaled epilogue, gn_rows not a multiple of the tile, groups not whole
+ * within a tile).  With a residual the statistics are those of residual + conv (the stored values). */
 int32_t vp2p_conv2d_gn_parts(const vp2p_conv_args* args);
 /* Workspace the shape wants for split-K (small-M shapes: fewer tiles than CUs); 0 = none. */
 int64_t vp2p_conv2d_workspace_bytes(const vp2p_conv_args* args);

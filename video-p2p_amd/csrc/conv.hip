@@ -791,7 +791,7 @@ static void one_pass_tile(const vp2p_conv_args* a, int64_t M, int* tbm, int* tbn
 
 extern "C" int32_t vp2p_conv2d_gn_parts(const vp2p_conv_args* a) {
   if (!a || !vp2p_conv2d_supported(a)) return 0;
-  if (a->epilogue != VP2P_CONV_EPI_NONE || a->residual || (a->alpha != 0.f && a->alpha != 1.f)) return 0;
+  if (a->epilogue != VP2P_CONV_EPI_NONE || (a->alpha != 0.f && a->alpha != 1.f)) return 0;
   if (conv::pick_ksplit(a) > 1) return 0;                       // statistics in the one-pass epilogue only
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   if (a->gn_groups <= 0 || a->cout % a->gn_groups || a->gn_rows <= 0 || M % a->gn_rows) return 0;

@@ -668,11 +668,13 @@ _CONV_GN_PARTS = {}   # (conv geometry, groups, rows) -> statistics partials per
 
 
 def conv2d_gn(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
-              img_add: Optional[torch.Tensor], groups: int, frames: int):
+              img_add: Optional[torch.Tensor], groups: int, frames: int, residual: Optional[torch.Tensor] = None):
     """K10 ``conv(x) + img_add[image]`` (the resnet's ``conv1(.) + temb``, resnet.py:146-156: two
     roundings) that also leaves the GroupNorm statistics of its output -- the next norm2's
     (resnet.py:158), ``groups`` groups over ``frames`` consecutive images -- as per-tile (count, mean,
-    M2) partials written by the epilogue, so the GroupNorm needs no statistics pass.  Returns
+    M2) partials written by the epilogue, so the GroupNorm needs no statistics pass.  ``residual``
+    (instead of ``img_add``): ``residual + conv(x)`` (the resnet's output, whose statistics the next
+    Transformer3DModel.norm takes, attention.py:110).  Returns
     (y, (partials, parts)), or None when the shape cannot produce them in one pass (split-K, tile /
     group geometry): the caller then runs the conv and the GroupNorm as usual."""
     if not x.is_contiguous(memory_format=torch.channels_last) or x.dtype != torch.bfloat16:
@@ -695,6 +697,12 @@ def conv2d_gn(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor
         return None
     y = torch.empty(shape, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
     partials = torch.empty((N // frames) * parts * groups * 3, device=x.device, dtype=torch.float32)
+    if residual is not None:
+        if img_add is not None or residual.shape != y.shape or residual.dtype != y.dtype:
+            return None
+        if not residual.is_contiguous(memory_format=torch.channels_last):
+            residual = residual.contiguous(memory_format=torch.channels_last)
+        a.residual = _ptr(residual)
     if img_add is not None:
         img_add = img_add.contiguous()
         a.img_add = _ptr(img_add)

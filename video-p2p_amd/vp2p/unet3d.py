@@ -37,6 +37,16 @@ class UNet3DConditionOutput:
         return getattr(self, k)
 
 
+# GroupNorm statistics a producer's epilogue already computed for the tensor it returned (id -> (tensor,
+# (partials, parts))); the consumer pops its entry, and UNet3DConditionModel.forward clears the rest
+_PENDING_STATS = {}
+
+
+def _take_stats(x: torch.Tensor):
+    hit = _PENDING_STATS.pop(id(x), None)
+    return hit[1] if hit is not None and hit[0] is x else None
+
+
 def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bool = False,
                       add: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None) -> torch.Tensor:
     """GroupNorm whose statistics span ``frames`` consecutive samples of a ``(b f) c h w``
@@ -204,20 +214,33 @@ class ResnetBlock3D(nn.Module):
             h = self.dropout(group_norm_frames(h, self.norm2, frames, silu=True, add=t))
         if self.output_scale_factor != 1.0:
             return (sc + self.conv2(h)) / self.output_scale_factor
+        nxt = self.__dict__.get("_next_norm")       # the GroupNorm that reads this output next, if known
+        if nxt is not None and self._conv_gn_ok(self.conv2, h, sc) and nxt.affine:
+            r = ops.conv2d_gn(h, self.conv2.weight, self.conv2.bias, 1, 1, None, nxt.num_groups, 1, residual=sc)
+            if r is not None:
+                _PENDING_STATS[id(r[0])] = r       # per-frame statistics for Transformer3DModel.norm
+                return r[0]
         return self.conv2(h, residual=sc)          # sc + conv2(h): the add fused into K10's epilogue
 
 
     def _conv1_gn_ok(self, hn, t) -> bool:
         """The fused conv1 + temb + norm2-statistics path: inference, bf16 K10 (the per-shape table
         picks K10 for conv1), a plain InflatedConv3d / GroupNorm pair, dropout inactive."""
-        c1, n2 = self.conv1, self.norm2
-        if autograd.needs_grad(hn, c1.weight, c1.bias, t, n2.weight, n2.bias) or (self.training and self.dropout.p):
+        n2 = self.norm2
+        if autograd.needs_grad(n2.weight, n2.bias) or (self.training and self.dropout.p) or not n2.affine:
             return False
-        if type(c1) is not InflatedConv3d or c1._forward_hooks or c1._forward_pre_hooks or not n2.affine:
+        return self._conv_gn_ok(self.conv1, hn, t)
+
+    @staticmethod
+    def _conv_gn_ok(conv, x, extra) -> bool:
+        """A plain 3x3 InflatedConv3d at inference on bf16 that the per-shape table puts on K10."""
+        if autograd.needs_grad(x, conv.weight, conv.bias, extra):
             return False
-        if hn.dtype != torch.bfloat16 or not hn.is_cuda or c1.kernel_size != (3, 3) or c1.stride != (1, 1):
+        if type(conv) is not InflatedConv3d or conv._forward_hooks or conv._forward_pre_hooks:
             return False
-        return ops.CONV.prefers_k10(hn, c1.weight, 1, 1)
+        if x.dtype != torch.bfloat16 or not x.is_cuda or conv.kernel_size != (3, 3) or conv.stride != (1, 1):
+            return False
+        return ops.CONV.prefers_k10(x, conv.weight, 1, 1)
 
 
 class GEGLU(nn.Module):
@@ -318,7 +341,12 @@ class Transformer3DModel(nn.Module):
 
     def forward(self, x, context, frames):
         Bf, C, H, W = x.shape
-        h = group_norm_frames(x, self.norm, 1)
+        st = _take_stats(x)          # per-frame statistics left by the resnet conv that produced x
+        if st is not None and not autograd.needs_grad(x, self.norm.weight, self.norm.bias):
+            n = self.norm
+            h = ops.group_norm_from_partials(x, n.num_groups, n.weight, n.bias, n.eps, 1, st)
+        else:
+            h = group_norm_frames(x, self.norm, 1)
         tok = h.permute(0, 2, 3, 1).reshape(Bf, H * W, C)
         tok = ops.linear(tok, self.proj_in.weight.view(self.proj_in.out_channels, -1), self.proj_in.bias)
         for blk in self.transformer_blocks:
@@ -384,6 +412,7 @@ class CrossAttnDownBlock3D(nn.Module):
     def forward(self, x, temb, ctx, frames):
         outs = ()
         for r, a in zip(self.resnets, self.attentions):
+            object.__setattr__(r, "_next_norm", a.norm)
             x = a(r(x, temb, frames), ctx, frames)
             outs += (x,)
         if self.downsamplers is not None:
@@ -419,6 +448,7 @@ class UNetMidBlock3DCrossAttn(nn.Module):
         self.attentions = nn.ModuleList([Transformer3DModel(heads, c // heads, c, ctx_dim)])
 
     def forward(self, x, temb, ctx, frames):
+        object.__setattr__(self.resnets[0], "_next_norm", self.attentions[0].norm)
         x = self.resnets[0](x, temb, frames)
         for a, r in zip(self.attentions, self.resnets[1:]):
             x = r(a(x, ctx, frames), temb, frames)
@@ -434,6 +464,8 @@ class _UpBlock(nn.Module):
 
     def forward(self, x, skips, temb, ctx, frames, upsample_size=None):
         for i, r in enumerate(self.resnets):
+            if self.attentions is not None:
+                object.__setattr__(r, "_next_norm", self.attentions[i].norm)
             x = r(x, temb, frames, skip=skips[-1 - i])           # cat([x, skip], dim=1), not materialised
             if self.attentions is not None:
                 x = self.attentions[i](x, ctx, frames)
@@ -577,6 +609,7 @@ class UNet3DConditionModel(nn.Module):
             off += n
 
     def _forward(self, sample, emb, ctx, return_dict):
+        _PENDING_STATS.clear()
         B, Cin, f, H, W = sample.shape
         x = sample.to(self.dtype).permute(0, 2, 1, 3, 4).reshape(B * f, Cin, H, W)
         x = self.conv_in(x.contiguous(memory_format=torch.channels_last))
@@ -593,6 +626,7 @@ class UNet3DConditionModel(nn.Module):
             size = skips[-1].shape[2:] if (forward_size and i < len(self.up_blocks) - 1) else None
             x = blk(x, res, emb, ctx, f, size)
         x = self.conv_out(group_norm_frames(x, self.conv_norm_out, f, silu=True))
+        _PENDING_STATS.clear()
         out = x.reshape(B, f, -1, H, W).permute(0, 2, 1, 3, 4)
         if not return_dict:
             return (out,)
