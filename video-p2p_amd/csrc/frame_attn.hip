@@ -563,7 +563,7 @@ static int launch_frame(const vp2p_frame_attn_args* a, hipStream_t stream) {
   using C = FrameCfg<T, D>;
   const int FQ = a->frames * a->tokens_q;
   if constexpr (C::BF && C::ONES && D <= 80) {
-    constexpr int KT = D <= 64 ? 256 : 64;
+    constexpr int KT = D <= 64 ? 256 : 64;   // d 80: 64-key tiles (32: 0.106, 128: 0.137 vs 0.103 ms, r04_k1_d80_kt_ab.jsonl)
     const int64_t nwg = (int64_t)a->batch * a->heads * ((FQ + 255) / 256);
     if (nwg <= 0 || nwg > 0x7fffffff) return VP2P_E_SHAPE;
 #ifndef VP2P_K1_LAB_X2F   // (lab builds only: x2f for every d = 40 launch, the A/B baseline)
