@@ -56,6 +56,8 @@ def test_conv2d(n, cin, h, w, cout, k, stride):
     (32, 320, 64, 64, 320, 3, 2, False),     # Downsample3D at res-64
     (32, 960, 32, 32, 640, 1, 1, True),      # conv_shortcut 1x1 + residual
     (8, 1920, 64, 64, 320, 3, 1, False),     # up-block concat input, 90 K-steps
+    (32, 320, 64, 64, 320, 3, 1, True),      # the edit's res-64 resnet conv (wide tile)
+    (16, 640, 32, 32, 640, 3, 1, False),     # res-32, 32-pixel rows
 ])
 def test_conv2d_large_m(n, cin, h, w, cout, k, stride, residual):
     """The 256-row, three-stage LDS-DMA form (conv_kernel_p: >= 256 tiles of 256 rows) against the
