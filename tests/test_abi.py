@@ -108,3 +108,48 @@ def test_linear_rule_table():
     r.rules = {"640|640": [[None, 4096], [65536, 65536], [131072, None]]}
     assert r.use_k10(10, 640, 640) and r.use_k10(4096, 640, 640) and not r.use_k10(8192, 640, 640)
     assert r.use_k10(65536, 640, 640) and not r.use_k10(100000, 640, 640) and r.use_k10(10 ** 7, 640, 640)
+
+
+def test_conv_gn_parts_host():
+    """vp2p_conv2d_gn_parts (ABI 15): the tiles per GroupNorm sample the epilogue writes partials for --
+    the one-pass tile's rows -- or 0 where the epilogue cannot produce them (host logic, no GPU)."""
+    import ctypes
+    from vp2p import _lib
+    lib = _lib.load()
+
+    def args(n, h, cin, cout, k=3):
+        a = _lib.ConvArgs(None, None, None, None, None, n, h, h, cin, cout, h, h, k, 1, (k - 1) // 2, _lib.BF16,
+                          _lib.CONV_EPI_NONE)
+        return a
+    a = args(32, 64, 320, 320)                    # the 8-frame edit's res-64 conv1: wide 256-row tile
+    a.gn_groups, a.gn_rows = 32, 8 * 64 * 64
+    assert lib.vp2p_conv2d_gn_parts(ctypes.byref(a)) == 8 * 64 * 64 // 256
+    a.gn_rows = 64 * 64                           # per-frame statistics (Transformer3DModel.norm)
+    assert lib.vp2p_conv2d_gn_parts(ctypes.byref(a)) == 16
+    a.residual = 16                               # conv2 + shortcut: statistics of the stored sum
+    assert lib.vp2p_conv2d_gn_parts(ctypes.byref(a)) == 16
+    a.residual = None
+    a.gn_groups = 7                               # groups must divide the channels
+    assert lib.vp2p_conv2d_gn_parts(ctypes.byref(a)) == 0
+    a.gn_groups, a.gn_rows = 32, 100              # rows per sample not a multiple of the tile
+    assert lib.vp2p_conv2d_gn_parts(ctypes.byref(a)) == 0
+    b = args(4, 8, 1280, 1280)                    # res-8, small M: split-K, no one-pass epilogue
+    b.gn_groups, b.gn_rows = 32, 64
+    assert lib.vp2p_conv2d_gn_parts(ctypes.byref(b)) == 0
+    c = args(32, 64, 320, 320)
+    c.img_add, c.residual = 16, 32                # a per-image add only without a residual
+    assert lib.vp2p_conv2d_supported(ctypes.byref(c)) == 0
+
+
+def test_geglu_interleave_layout():
+    """K10's GEGLU weight order: per 32 rows, 16 value rows then the matching 16 gate rows."""
+    import torch
+    from vp2p import ops
+    inner, k = 160, 4
+    w = torch.arange(2 * inner * k, dtype=torch.float32).reshape(2 * inner, k)
+    b = torch.arange(2 * inner, dtype=torch.float32)
+    wi, bi = ops.geglu_interleave(w, b)
+    for blk in range(inner // 16):
+        assert torch.equal(wi[32 * blk:32 * blk + 16], w[16 * blk:16 * blk + 16])
+        assert torch.equal(wi[32 * blk + 16:32 * blk + 32], w[inner + 16 * blk:inner + 16 * blk + 16])
+        assert torch.equal(bi[32 * blk + 16:32 * blk + 32], b[inner + 16 * blk:inner + 16 * blk + 16])
