@@ -290,6 +290,10 @@ int vp2p_group_norm_merge(const vp2p_group_norm_args* args, const float* partial
  * the (batch, groups, 3) triples of a frame-sharded exchange. */
 int vp2p_group_norm_finalize_parts(const vp2p_group_norm_args* args, const float* partials, int32_t parts,
                                    float* stats, void* stream);
+/* The apply of vp2p_group_norm_apply on such partials, merged inside every apply block (one launch:
+ * cheaper than _finalize_parts + _apply_stats at small part counts). */
+int vp2p_group_norm_apply_parts(const vp2p_group_norm_args* args, const float* partials, int32_t parts,
+                                void* stream);
 int vp2p_group_norm_merge_parts(const vp2p_group_norm_args* args, const float* partials, int32_t parts,
                                 float* triples, void* stream);
 int vp2p_group_norm_finalize_merged(const vp2p_group_norm_args* args, const float* triples, int32_t nsets,

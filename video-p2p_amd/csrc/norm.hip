@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const vp2p_group_norm_
 // partials itself (the ABI's vp2p_group_norm_apply)
 template <typename T, bool ADD, bool SILU, bool FIN = false>
 __global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_args a, const GnGeom g,
-                                                        const float* __restrict__ partials, int nsets) {
+                                                        const float* __restrict__ partials, int nsets, int mparts) {
   __shared__ float s_w[FIN ? 1 : 3 * 512];
   __shared__ float s_mean[64], s_rstd[64];
   const int C = a.channels, G = a.groups, R = g.R, nvec = g.nvec, cg = g.cg;
@@ -271,10 +271,11 @@ __global__ __launch_bounds__(512) void gn_apply_kernel(const vp2p_group_norm_arg
     const int gi = tid / tpg, k = tid - gi * tpg;
     Welford w = {0.f, 0.f, 0.f};
     if (gi < G) {
-      const int total = nsets * g.parts;
+      const int P = mparts > 0 ? mparts : g.parts;     // partials per (set, sample): _stats' or a producer's
+      const int total = nsets * P;
       for (int e = k; e < total; e += tpg) {
-        const int set = e / g.parts, p = e - set * g.parts;
-        const float* q = partials + ((((int64_t)set * a.batch + b) * g.parts + p) * G + gi) * 3;
+        const int set = e / P, p = e - set * P;
+        const float* q = partials + ((((int64_t)set * a.batch + b) * P + p) * G + gi) * 3;
         w = wmerge(w, {q[0], q[1], q[2]});
       }
     }
@@ -358,13 +359,13 @@ static void gn_stats_launch(const vp2p_group_norm_args& a, const GnGeom& g, hipS
 // parts = the partial sets (FIN = false) or the finalized (batch, groups, 2) statistics (FIN = true)
 template <typename T, bool FIN = false>
 static void gn_apply_launch(const vp2p_group_norm_args& a, const GnGeom& g, const float* parts, int nsets,
-                            hipStream_t s) {
+                            hipStream_t s, int mparts = 0) {
   const dim3 grid(g.parts, a.batch), block(g.threads);
   const bool add = a.add != nullptr, silu = a.silu != 0;
-  if (add && silu) hipLaunchKernelGGL((gn_apply_kernel<T, true, true, FIN>), grid, block, 0, s, a, g, parts, nsets);
-  else if (add) hipLaunchKernelGGL((gn_apply_kernel<T, true, false, FIN>), grid, block, 0, s, a, g, parts, nsets);
-  else if (silu) hipLaunchKernelGGL((gn_apply_kernel<T, false, true, FIN>), grid, block, 0, s, a, g, parts, nsets);
-  else hipLaunchKernelGGL((gn_apply_kernel<T, false, false, FIN>), grid, block, 0, s, a, g, parts, nsets);
+  if (add && silu) hipLaunchKernelGGL((gn_apply_kernel<T, true, true, FIN>), grid, block, 0, s, a, g, parts, nsets, mparts);
+  else if (add) hipLaunchKernelGGL((gn_apply_kernel<T, true, false, FIN>), grid, block, 0, s, a, g, parts, nsets, mparts);
+  else if (silu) hipLaunchKernelGGL((gn_apply_kernel<T, false, true, FIN>), grid, block, 0, s, a, g, parts, nsets, mparts);
+  else hipLaunchKernelGGL((gn_apply_kernel<T, false, false, FIN>), grid, block, 0, s, a, g, parts, nsets, mparts);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -822,6 +823,18 @@ extern "C" int vp2p_group_norm_merge(const vp2p_group_norm_args* a, const float*
   if (!partials || !triples) return VP2P_E_ARG;
   hipLaunchKernelGGL(gn_finalize_kernel<true>, dim3(a->groups, a->batch), dim3(256), 0,
                      static_cast<hipStream_t>(stream), *a, g, partials, 1, triples);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+extern "C" int vp2p_group_norm_apply_parts(const vp2p_group_norm_args* a, const float* partials, int32_t parts,
+                                           void* stream) {
+  GnGeom g;
+  int rc = gn_check(a, &g);
+  if (rc != VP2P_OK) return rc;
+  if (!partials || parts <= 0) return VP2P_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a->dtype == VP2P_BF16) gn_apply_launch<bf16>(*a, g, partials, 1, s, parts);
+  else gn_apply_launch<float>(*a, g, partials, 1, s, parts);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 

@@ -30,7 +30,8 @@ EXPORTS = ("vp2p_frame_attn_fwd", "vp2p_cross_kv_workspace_bytes", "vp2p_cross_k
            "vp2p_nulltext_loss", "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
            "vp2p_add_layer_norm_fwd", "vp2p_conv2d_workspace_bytes", "vp2p_group_norm_finalize",
            "vp2p_group_norm_apply_stats", "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged",
-           "vp2p_group_norm_finalize_parts", "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts")
+           "vp2p_group_norm_finalize_parts", "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts",
+           "vp2p_group_norm_apply_parts")
 
 
 class GroupNormArgs(ctypes.Structure):
@@ -181,6 +182,7 @@ def load(path: str = None):
     lib.vp2p_conv2d_gn_parts.argtypes = [POINTER(ConvArgs)]
     lib.vp2p_group_norm_finalize_parts.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p]
     lib.vp2p_group_norm_merge_parts.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p]
+    lib.vp2p_group_norm_apply_parts.argtypes = [gn, c_void_p, c_int32, c_void_p]
     lib.vp2p_conv2d_workspace_bytes.restype = c_int64
     lib.vp2p_add_layer_norm_fwd.argtypes = [POINTER(LayerNormArgs), c_void_p, c_void_p, c_void_p]
     for name in ("vp2p_frame_attn_fwd", "vp2p_cross_kv_prep", "vp2p_cross_attn_p2p_fwd",
@@ -192,7 +194,7 @@ def load(path: str = None):
                  "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
                  "vp2p_add_layer_norm_fwd", "vp2p_group_norm_finalize", "vp2p_group_norm_apply_stats",
                  "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged", "vp2p_group_norm_finalize_parts",
-                 "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts"):
+                 "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts", "vp2p_group_norm_apply_parts"):
         getattr(lib, name).restype = c_int32
     if lib.vp2p_abi_version() != ABI_VERSION:
         raise Vp2pError(f"{p}: ABI version {lib.vp2p_abi_version()} != {ABI_VERSION}; rebuild")

@@ -731,6 +731,9 @@ def group_norm_from_partials(x: torch.Tensor, num_groups: int, weight: Optional[
         tri = shard.all_gather_flat(tri)
         check(lib.vp2p_group_norm_finalize_merged(ctypes.byref(a), _ptr(tri), shard.world, _ptr(st), s),
               "vp2p_group_norm_finalize_merged")
+    elif parts < GN_FINALIZE_MIN_PARTS:       # few partials: every apply block merges them (one launch)
+        check(lib.vp2p_group_norm_apply_parts(ctypes.byref(a), _ptr(partials), parts, s), "vp2p_group_norm_apply_parts")
+        return out
     else:
         check(lib.vp2p_group_norm_finalize_parts(ctypes.byref(a), _ptr(partials), parts, _ptr(st), s),
               "vp2p_group_norm_finalize_parts")
