@@ -210,10 +210,11 @@ __device__ __forceinline__ float erf_fast(float x) {
   return copysignf(1.f - __builtin_amdgcn_rcpf(p), x);
 }
 
-// EPI = 0: bf16 output (+ residual).  EPI = 1 (GEGLU, 1x1 only): the weight rows come interleaved
-// per 16 as [8 "a" rows, the 8 matching "gate" rows], and the epilogue writes
-// y[p, (col / 16) * 8 + col % 8] = a * gelu(g) (erf to 1.8e-6, each step rounded to bf16 as torch's
-// eager GEGLU does) into a (M, cout/2) output from the accumulators.  EPI = 2: split-K slice, fp32 accumulators to workspace[split].
+// EPI = 0: bf16 output (+ residual, or + a per-image vector; optionally the GroupNorm partials of the
+// stored tile).  EPI = 1 (GEGLU, 1x1 only): the weight rows come interleaved per 32 as [16 value
+// rows | the 16 matching gate rows] (GCfgG), and the epilogue writes y[p, c] = value * gelu(gate) of
+// channel c (erf to 1.8e-6, each step rounded to bf16 as torch's eager GEGLU does) into a (M, cout/2)
+// output.  EPI = 2: split-K slice, fp32 accumulators to workspace[split].
 // AM (addressing): 1 = 32-bit buffer offsets precomputed per DMA row (input below 2^31 bytes): the
 // per-step address is one add + the padding mask; 2 = the same with the x2 nearest upsample read on
 // the fly (per row: the source pixel's offset and the output pixel's parities; a tap's source row /
@@ -465,7 +466,7 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   const bf16* bias = static_cast<const bf16*>(a.bias);
   if constexpr (EPI == 1) {
     // GEGLU straight from the accumulators: tile 2q of the wave holds the values and tile 2q + 1 the
-    // gates of the same 16 channels (weights interleaved per 16), so lane l has a channel's value and
+    // gates of the same 16 channels (weights interleaved per 32 rows), so lane l has a channel's value and
     // gate for rows 4 * fq + e, e = 0..3, and forms those four outputs on packed FP32 -- the
     // projection rounded to bf16, gelu rounded, the product rounded, exactly K9's order.  The
     // (TBM, TBN / 2) output tile is staged in LDS (free after the last K-step) and leaves as whole
