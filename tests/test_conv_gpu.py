@@ -267,3 +267,23 @@ def test_conv2d_gn_stats(n, frames, c, h, cout, groups):
     err = (got.float() - f32).abs().max().item() / f32.abs().max().item()
     assert err < 1e-2, err
     assert (got.float() - want.float()).abs().max().item() <= 2 * (want.float() - f32).abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("n,c,h,cout", [(32, 1280, 8, 1280),     # split-K: the add in the reduce pass
+                                         (8, 320, 64, 320),      # one pass
+                                         (4, 640, 32, 640)])     # short tile
+def test_conv2d_img_add(n, c, h, cout):
+    """K10 conv + a per-image vector (ABI 15 img_add: the resnet's h + temb) equals the conv then the
+    add, bit for bit (two roundings), on the one-pass, short and split-K forms."""
+    from vp2p import ops
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(n, c, h, h, generator=g).to(torch.bfloat16).to(DEV).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(cout, c, 3, 3, generator=g) / (c * 9) ** 0.5).to(torch.bfloat16).to(DEV)
+    w = w.contiguous(memory_format=torch.channels_last)
+    b = (torch.randn(cout, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    t = (torch.randn(n, cout, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    with torch.no_grad():
+        y = ops.conv2d(x, w, b, 1, 1, img_add=t)
+        ref = (ops.conv2d(x, w, b, 1, 1).float() + t.float()[:, :, None, None]).to(torch.bfloat16)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)

@@ -630,10 +630,12 @@ _CONV_WS = {}       # conv geometry -> split-K workspace bytes (a pure function 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
            padding: int = 0, residual: Optional[torch.Tensor] = None, upsample: bool = False,
-           x2: Optional[torch.Tensor] = None) -> torch.Tensor:
+           x2: Optional[torch.Tensor] = None, img_add: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K10: nn.Conv2d on channels-last bf16 with the bias and an optional residual add fused
-    (``residual + conv(x)``, the resnet shortcut add of resnet.py:196-205).  Returns a channels-last
-    (N, Cout, Ho, Wo) tensor.  Raises for shapes K10 does not cover (see ``conv2d_supported``)."""
+    (``residual + conv(x)``, the resnet shortcut add of resnet.py:196-205) or a per-image vector
+    added after the bias (``img_add`` (N, Cout): the resnet's h + temb, resnet.py:149-156).  Returns a
+    channels-last (N, Cout, Ho, Wo) tensor.  Raises for shapes K10 does not cover (see
+    ``conv2d_supported``)."""
     if not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv2d: x must be channels-last contiguous")
     w = weight if weight.is_contiguous(memory_format=torch.channels_last) else \
@@ -650,6 +652,11 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
         if not residual.is_contiguous(memory_format=torch.channels_last):
             residual = residual.contiguous(memory_format=torch.channels_last)
         a.residual = _ptr(residual)
+    if img_add is not None:
+        if tuple(img_add.shape) != (shape[0], shape[1]) or img_add.dtype != y.dtype:
+            raise ValueError("conv2d: img_add must be (N, Cout) of the output dtype")
+        img_add = img_add.contiguous()
+        a.img_add = _ptr(img_add)
     a.y = _ptr(y)
     lib = _lib.load()
     wkey = (a.batch, a.in_h, a.in_w, a.cin, a.cout, a.kernel, a.stride, a.pad, a.upsample, a.cin2, a.epilogue)
