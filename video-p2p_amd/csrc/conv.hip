@@ -712,6 +712,9 @@ static double wave_fill(int64_t tiles, int64_t slots) {
 }
 
 static int pick_tile(const vp2p_conv_args* a, int64_t M) {
+#ifdef VP2P_K10_FORCE_CF   // lab A/B builds only (tools/lab_build.sh)
+  if (VP2P_K10_FORCE_CF != 2 || a->cout % 320 == 0) return VP2P_K10_FORCE_CF;
+#endif
   const int64_t tiles_b = (M + 255) / 256 * (a->cout / BN);
   const int64_t tiles_0 = (M + GBM - 1) / GBM * (a->cout / BN);
   const bool wide_ok = a->cout % 320 == 0;    // plain and GEGLU epilogues (GEGLU: profiles/r03_k10_geglu_wide_ab.jsonl)
