@@ -742,8 +742,12 @@ static int pick_ksplit(const vp2p_conv_args* a) {
   const int64_t tiles = (M + GBM - 1) / GBM * (a->cout / BN);
   const int nsteps = a->kernel * a->kernel * (a->cin / BK);
   if (tiles >= 384) return 1;
+  // at most 8 slices, 16 where 8 would leave half the CUs without a workgroup (<= 16 tiles: the
+  // 8x8-latent convs of a 1-frame clip; profiles/r04_k10_ksplit16.jsonl: M 256 K 2560*9 N 1280
+  // 46.1 -> 35.0 us, K 1280*9 29.1 -> 25.4 us; 16 slices of the 32-tile grids measured slower)
+  const int cap = tiles <= 16 ? 16 : 8;
   int k = (int)((512 + tiles - 1) / tiles);
-  if (k > 8) k = 8;
+  if (k > cap) k = cap;
   while (k > 1 && nsteps / k < 8) --k;                          // keep >= 8 steps per slice
   return k;
 }
