@@ -52,11 +52,13 @@ def _prescale(q, d):
 
 @pytest.mark.parametrize("prescaled", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("d,frames,n", [(40, 3, 200), (80, 2, 256), (160, 2, 144), (40, 8, 64), (40, 2, 300)])
+@pytest.mark.parametrize("d,frames,n", [(40, 3, 200), (80, 2, 256), (160, 2, 144), (40, 8, 64), (40, 2, 300),
+                                         (40, 2, 128), (40, 2, 256)])
 def test_frame_attention(dtype, d, frames, n, prescaled):
     """Both query conventions: plain q (scale applied in the kernel) and q pre-multiplied by
     scale*log2(e) (the production call, FrameAttention.forward; at d = 40 bf16 it selects the
-    folded-max kernel, whose ragged 128-key tiles n = 200 / 64 / 300 exercise)."""
+    folded-max kernel, whose ragged 128-key tiles n = 200 / 64 / 300 exercise; key counts that are
+    multiples of 256 -- n = 128 / 256: one and two tiles -- take the res-64 pp kernel)."""
     from vp2p import ops
     heads, B = 8, 2
     C = heads * d

@@ -1,6 +1,7 @@
 // K1 at res-64 -- FrameAttention with first-frame K/V (tuneavideo/models/attention.py:282-322) in
 // the form the UNet calls it there: bf16, head_dim 40, q pre-scaled by scale * log2(e) (the to_q
-// GEMM's alpha), tokens_kv a multiple of 128.  These launches carry 88 % of K1's FLOPs.
+// GEMM's alpha), tokens_kv a multiple of 256 (other lengths: the x2f kernel).  These launches
+// carry 88 % of K1's FLOPs.
 //
 // Why a separate kernel: at d = 40 a 32x32 score block is 7 MFMAs (3 QK^T k-steps, 4 PV) against
 // 16 v_exp + 8 v_cvt per lane, so the SIMD's issue port -- not the matrix pipe -- is the tight
@@ -17,7 +18,7 @@
 //    keeps it there); scores, P, Q and the K/V fragments fit the arch VGPRs;
 //  * each K / V^T fragment is re-read as soon as its last MFMA of the block has issued, >= 5 MFMA
 //    slots before its next use;
-//  * K and V tiles of 128 keys arrive by LDS-DMA (buffer_load ... lds, 32-bit offsets, no register
+//  * K and V tiles of 256 keys arrive by LDS-DMA (buffer_load ... lds, 32-bit offsets, no register
 //    staging) in dense 80-byte rows, through a 3-slot ring with ONE barrier per tile: tile t+2 is
 //    issued right after tile t's barrier, the first point where every wave is done with tile t-1;
 //  * the padding the MFMAs need is never stored: the K fragment of columns 40..47 (the folded -m
@@ -46,15 +47,23 @@ typedef __attribute__((address_space(3))) char lchar;
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kD = 40, kKT = 128, kRowB = kD * 2;                 // dense K / V rows: 80 bytes
-constexpr int kSlotB = kKT * kRowB;                               // 10 KiB per K or V slot
+// 256-key tiles: one barrier and one row-sum check per eight blocks; measured 0.7655 vs 0.780 ms
+// (median) against 128-key tiles at res-64 B4 f8, same output (profiles/r04_k1_pp_kt256.jsonl)
+#ifndef VP2P_K1_PP_KT
+#define VP2P_K1_PP_KT 256
+#endif
+constexpr int kD = 40, kKT = VP2P_K1_PP_KT, kRowB = kD * 2;        // dense K / V rows: 80 bytes
+constexpr int kNB = kKT / 32;                                      // 32-key blocks per tile
+constexpr int kSlotB = kKT * kRowB;                               // 20 KiB per K or V slot
 constexpr int kNSlot = 3;
-constexpr int kChunks = kKT * kD / 8;                             // 16-byte chunks per tile: 640
-constexpr int kDmaPerTile = kChunks / 64;                          // wave-instructions per tile: 10
+constexpr int kChunks = kKT * kD / 8;                             // 16-byte chunks per tile: 1280
+constexpr int kDmaPerTile = kChunks / 64;                          // wave-instructions per tile: 20
 static_assert(kChunks % 64 == 0, "whole DMA instructions");
-// LDS: K ring, V ring, constant replicas [1, 0 x 7] at kCR + 64 + 640 k (k = 0..15)
+// LDS: K ring, V ring, constant replicas [1, 0 x 7] at kCR + 64 + 640 k (k < kRep: one per 8 key
+// rows, where the K / V^T fragment reads of any block's padding land)
 constexpr int kKRing = 0, kVRing = kNSlot * kSlotB, kCR = 2 * kNSlot * kSlotB;
-constexpr int kLdsBytes = kCR + 64 + 640 * 15 + 16;
+constexpr int kRep = kKT / 8;
+constexpr int kLdsBytes = kCR + 64 + 640 * (kRep - 1) + 16;
 
 __device__ __forceinline__ bf16x8 ld128(const lchar* p) { return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(p); }
 __device__ __forceinline__ bf16x4 ldtr(const lchar* p) {
@@ -174,7 +183,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(co
   };
 
   // constant replicas, then tiles 0 and 1
-  if (tid < 16) {
+  if (tid < kRep) {
     u32x4 c1 = {__builtin_bit_cast(uint16_t, (T)1.0f), 0u, 0u, 0u};
     *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(L + kCR + 64 + 640 * tid) = c1;
   }
@@ -343,13 +352,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(co
     asm volatile("" : "+v"(k2b0), "+v"(k2b1), "+v"(v1b));
     block(kb0, k2b0, 32, vb, v1b, 0);
     // tile t+1 (issued a tile ago) has landed; every wave is done with tile t-1's slot (K last read
-    // in iteration 4t-2, V in 4t-1)
+    // in iteration kNB*t-2, V in kNB*t-1)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     dma_tile(t + 2);
-    block(kb0, k2b0, 64, vb, v1b, 32);
-    block(kb0, k2b0, 96, vb, v1b, 64);
-    block(kb1, k2b1, 0, vb, v1b, 96);
+#pragma unroll
+    for (int j = 1; j < kNB - 1; ++j) block(kb0, k2b0, 32 * (j + 1), vb, v1b, 32 * j);
+    block(kb1, k2b1, 0, vb, v1b, 32 * (kNB - 1));
     // once per tile: the row-sum growth check.  O holds blocks <= 4t+2; P (block 4t+3) and
     // S[0..SETS-2] (block 4t+4) are still at the old m; S[SETS-1] is recomputed with the new fold.
     sb();
