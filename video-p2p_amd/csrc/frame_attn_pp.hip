@@ -25,7 +25,7 @@
 //    column: Q'[40] = -m, K[40] = 1) and V^T rows 40..63 (row 40 all ones = the row sum) are read by
 //    the lanes that own them from 16 replicas of one 16-byte constant, placed where the fragment
 //    reads' immediate offsets land (broadcast reads, no per-read select);
-//  * the row-sum growth check of x2f runs once per tile; when it moves m it also rescales the work
+//  * the row-sum growth check of x2f runs once per two tiles; when it moves m it also rescales the work
 //    still in flight (every set's packed P, the next block's scores), so every term enters O at one
 //    scale (CDNA guide T13 hazard).
 #include "frame_attn.hpp"
@@ -359,8 +359,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void frame_attn_kernel_pp(co
 #pragma unroll
     for (int j = 1; j < kNB - 1; ++j) block(kb0, k2b0, 32 * (j + 1), vb, v1b, 32 * j);
     block(kb1, k2b1, 0, vb, v1b, 32 * (kNB - 1));
-    // once per tile: the row-sum growth check.  O holds blocks <= 4t+2; P (block 4t+3) and
-    // S[0..SETS-2] (block 4t+4) are still at the old m; S[SETS-1] is recomputed with the new fold.
+    // the row-sum growth check, at the end of every second tile (512 keys): 0.757-0.769 vs
+    // 0.784-0.788 ms with one per tile, same output (profiles/r04_k1_pp_check_every.jsonl; one per
+    // 1024 keys or none measured level with this).  Fewer checks only let p grow further before m
+    // moves -- more range, the same relative precision; a row that overflows still ends in the exact
+    // per-row fallback below.  At a check O holds blocks <= kNB(t+1)-2; P (block kNB(t+1)-1) and
+    // S[0..SETS-2] (block kNB(t+1)) are still at the old m; S[SETS-1] is recomputed with the new fold.
+    if ((t & 1) == 0) continue;
     sb();
     o_fence();
     float lc[SETS];
