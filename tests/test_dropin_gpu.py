@@ -72,9 +72,24 @@ class CrossAttention(nn.Module):
         return t.reshape(bh // HEADS, HEADS, n, d).permute(0, 2, 1, 3).reshape(bh // HEADS, n, HEADS * d)
 
 
+class FrameAttention(CrossAttention):
+    """Foreign attn1: the reference's subclass (attention.py:273-329) -- named ``FrameAttention``,
+    with its diffusers attributes group_norm / added_kv_proj_dim unset (as in SD-1.5) and the
+    xformers switch the pipeline toggles.  Its own forward must never run once registered."""
+
+    def __init__(self, w):
+        super().__init__(w)
+        self.group_norm, self.added_kv_proj_dim = None, None
+        self._use_memory_efficient_attention_xformers = True
+
+    def forward(self, *a, **k):
+        raise AssertionError("the reference FrameAttention.forward ran: attn1 was not routed to K1")
+
+
 class Block(nn.Module):
     def __init__(self, i):
         super().__init__()
+        self.attn1 = FrameAttention(_weights(i, 2, C))
         self.attn2 = CrossAttention(_weights(i, 0, CTX))
         self.attn_temp = CrossAttention(_weights(i, 1, C))
 
@@ -213,3 +228,47 @@ def test_foreign_controller_generic_path():
             rt, _ = O.hooked_forward(xt, None, wt, HEADS, oracle_ctrl, PLACES[bi])
             assert _rel(oc.cpu().numpy(), rc) < 1e-4 and _rel(ot.cpu().numpy(), rt) < 1e-4
     assert ctrl.cur_att_layer == 6 and len(ctrl.sums) == 6
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_frame_attention_on_foreign_tree(tokenizer, dtype):
+    """attn1 of a foreign tree (class named ``FrameAttention``, the reference's attn1) runs on K1
+    once registered: ``ops.frame_attention`` launches for every call, the controller's layer count
+    stays 32 (attn1 is not hooked, ptp_utils.py:237), and the output -- to_q, K/V of frame 0,
+    softmax, to_out (attention.py:282-329) -- matches the oracle within the north-star bars (fp32
+    1e-4, bf16 2e-2 of max|ref|) at res-64-like (1040 tokens), res-16 and res-8 token counts."""
+    import types
+    import vp2p
+    from vp2p import ops
+    net = ForeignUNet().cuda().to(dtype)
+    ctrl, _ = _controllers(tokenizer, False)
+    vp2p.register_attention_control(types.SimpleNamespace(unet=net), ctrl)
+    assert ctrl.num_att_layers == 32
+    calls = []
+    orig = ops.frame_attention
+
+    def counting(*a, **k):
+        calls.append(a[0].shape)
+        return orig(*a, **k)
+
+    ops.frame_attention = counting
+    try:
+        with torch.no_grad():
+            for bi in (0, 4, 6):
+                n = LEVELS[bi]
+                x = _rng(55, bi).standard_normal((B * F_, n, C)).astype(np.float32)
+                xt = torch.from_numpy(x).to(dtype)
+                got = net.blocks[bi].attn1(xt.cuda(), video_length=F_).float().cpu().numpy()
+                w = _weights(bi, 2, C)
+                xr = xt.float().numpy()
+                q = xr @ w["to_q"].T
+                k = xr @ w["to_k"].T
+                v = xr @ w["to_v"].T
+                o = O.frame_attention(q.astype(np.float32), k.astype(np.float32), v.astype(np.float32),
+                                      F_, HEADS)
+                ref = o @ w["to_out_w"].T + w["to_out_b"]
+                assert _rel(got, ref) < (1e-4 if dtype == torch.float32 else 2e-2), (bi, _rel(got, ref))
+    finally:
+        ops.frame_attention = orig
+    assert len(calls) == 3
+    assert ctrl.cur_att_layer == 0        # attn1 never reaches the controller

@@ -57,8 +57,9 @@ def _prescale(q, d):
 def test_frame_attention(dtype, d, frames, n, prescaled):
     """Both query conventions: plain q (scale applied in the kernel) and q pre-multiplied by
     scale*log2(e) (the production call, FrameAttention.forward; at d = 40 bf16 it selects the
-    folded-max kernel, whose ragged 128-key tiles n = 200 / 64 / 300 exercise; key counts that are
-    multiples of 256 -- n = 128 / 256: one and two tiles -- take the res-64 pp kernel)."""
+    folded-max kernel, whose ragged 128-key tiles n = 200 / 64 / 300 exercise; n = 256, a multiple
+    of the pp kernel's 256-key tile, takes the res-64 pp kernel as a single tile, n = 128 the x2f
+    kernel: several pp tiles are test_frame_attention_pp_tiles)."""
     from vp2p import ops
     heads, B = 8, 2
     C = heads * d
@@ -78,6 +79,37 @@ def test_frame_attention(dtype, d, frames, n, prescaled):
     out0 = ops.frame_attention(q.to(DEV), k0, v0, frames, heads, q_prescaled=prescaled)
     torch.cuda.synchronize()
     assert torch.equal(out0, out)
+
+
+@pytest.mark.parametrize("n,spikes", [(1024, (300, 900)), (4096, (300, 1380)), (4096, ())])
+def test_frame_attention_pp_tiles(n, spikes):
+    """The res-64 pp kernel (bf16, d = 40, pre-scaled q, 256-key tiles) over 4 and 16 tiles: its
+    3-slot LDS ring wraps (tile t + 2 lands in tile t - 1's slot) and its XOR-swizzled image is read
+    at every block offset.  Spike keys in tile 1 and in tile 3 / 5 make the row-sum growth check
+    move m part-way through the key axis, rescaling the in-flight P and S (the check runs after
+    every second tile).  float64 oracle on the same bf16 inputs, 2e-2 of max|ref|, plus the lse."""
+    from vp2p import ops
+    heads, B, frames, d = 2, 1, 2, 40
+    C = heads * d
+    q = _rand((B * frames, n, C), 11, 1.0)
+    k = _rand((B, n, C), 12, 1.0)
+    for i, key in enumerate(spikes):
+        k[0, key] *= 6.0 + 4.0 * i
+    v = _rand((B, n, C), 13, 1.0)
+    q, k, v = (x.to(torch.bfloat16) for x in (q, k, v))
+    q, qref = _prescale(q, d)
+    ref = O.frame_attention(qref, _np(k), _np(v), frames, heads)
+    assert np.isfinite(ref).all()
+    lse = torch.empty(B * heads, frames * n, device=DEV)
+    out = ops.frame_attention(q.to(DEV), k.to(DEV), v.to(DEV), frames, heads, lse=lse, q_prescaled=True)
+    torch.cuda.synchronize()
+    assert _rel(_np(out), ref) < 2e-2, _rel(_np(out), ref)
+    qd = np.asarray(qref, np.float64).reshape(B, frames * n, heads, d).transpose(0, 2, 1, 3)
+    kd = _np(k).astype(np.float64).reshape(B, n, heads, d).transpose(0, 2, 1, 3)
+    sc = qd @ kd.transpose(0, 1, 3, 2) * d ** -0.5 * np.log2(np.e)
+    mx = sc.max(-1, keepdims=True)
+    lse_ref = (mx[..., 0] + np.log2(np.exp2(sc - mx).sum(-1))).reshape(B * heads, frames * n)
+    assert np.abs(lse.cpu().numpy() - lse_ref).max() < 5e-2
 
 
 def test_frame_attention_large_logits():

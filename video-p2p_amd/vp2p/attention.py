@@ -401,9 +401,32 @@ class DummyController:
         return None
 
 
+def _frame_forward(net):
+    """Forward for a foreign module whose class is named ``FrameAttention`` (the reference's attn1,
+    tuneavideo/models/attention.py:273-329, signature :274): the same K1 path as ours
+    (``FrameAttention.forward``), on the module's own to_q / to_k / to_v / to_out, heads and scale.
+    The reference's xformers / sliced-attention switches select among equal maths there and are
+    ignored here; the options its UNet never uses raise, as ours do."""
+    def forward(hidden_states, encoder_hidden_states=None, attention_mask=None, video_length=None,
+                residual=None):
+        if getattr(net, "group_norm", None) is not None or getattr(net, "added_kv_proj_dim", None) is not None:
+            raise NotImplementedError("FrameAttention: group_norm / added_kv_proj_dim")
+        if video_length is None:
+            raise ValueError("FrameAttention needs video_length (attention.py:293)")
+        return FrameAttention.forward(net, hidden_states, encoder_hidden_states, attention_mask,
+                                      video_length, residual)
+    return forward
+
+
 def register_attention_control(model, controller):
     """ptp_utils.py:188-255: patch every module whose class is named ``CrossAttention`` under the
-    UNet's down*/up*/mid* children; set ``controller.num_att_layers``."""
+    UNet's down*/up*/mid* children; set ``controller.num_att_layers``.
+
+    Beyond the reference: modules whose class is named ``FrameAttention`` (attn1, which the
+    reference's hook never reaches: its class name differs, ptp_utils.py:237) are routed to K1
+    too, so the reference's own UNet runs every attention on the kernels.  They are not hooked by
+    the controller (the reference edits only attn2 / attn_temp) and are not counted in
+    ``num_att_layers`` (32 for SD-1.5, as the reference counts)."""
     ctrl = DummyController() if controller is None else controller
 
     def make_forward(net, place):
@@ -418,6 +441,10 @@ def register_attention_control(model, controller):
         if net.__class__.__name__ == "CrossAttention":
             net.forward = make_forward(net, place)
             return count + 1
+        if net.__class__.__name__ == "FrameAttention":
+            if not isinstance(net, FrameAttention):        # ours already runs on K1
+                net.forward = _frame_forward(net)
+            return count
         for child in net.children():
             count = walk(child, count, place)
         return count

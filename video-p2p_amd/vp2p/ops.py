@@ -812,12 +812,13 @@ class ConvSelector:
             return k10()
         return lib()
 
-    def prefers_k10(self, x, weight, stride: int, padding: int) -> bool:
-        """Whether ``run`` would take K10 for this plain convolution (no residual, upsample or second
-        source) -- without running anything ("tune" mode: no, it times on first use)."""
+    def prefers_k10(self, x, weight, stride: int, padding: int, residual: bool = False) -> bool:
+        """Whether ``run`` would take K10 for this convolution (no upsample or second source; with
+        or without a residual add: the same table key ``run`` builds) -- without running anything
+        ("tune" mode: no, it times on first use)."""
         if self.mode == "tune":
             return False
-        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, False, False)
+        key = ("conv", tuple(x.shape), tuple(weight.shape), stride, padding, bool(residual), False)
         skey = (key, False, x.dtype, weight.dtype, x.is_cuda, x.is_contiguous(memory_format=torch.channels_last), True)
         sup = self._supported.get(skey)
         if sup is None:

@@ -47,11 +47,21 @@ def _take_stats(x: torch.Tensor):
     return hit[1] if hit is not None and hit[0] is x else None
 
 
+def clip_shard(per_frame: bool = False):
+    """The FrameShard a clip-spanning GroupNorm merges its statistics over (None: not sharded).
+    ``per_frame``: the norm's statistics are per image (Transformer3DModel.norm, attention.py:71),
+    never merged -- decided by the norm, not by how many frames this rank holds, which can be one."""
+    return None if per_frame else frame_parallel.active()
+
+
 def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bool = False,
-                      add: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      add: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None,
+                      per_frame: bool = False) -> torch.Tensor:
     """GroupNorm whose statistics span ``frames`` consecutive samples of a ``(b f) c h w``
-    channels-last tensor (frames=1: the per-frame GroupNorm of Transformer3DModel.norm), applied
-    to ``x + add[:, :, None, None]`` when ``add`` ((b f), c) is given, then optionally SiLU (K7).
+    channels-last tensor (``per_frame`` with frames=1: the per-frame GroupNorm of
+    Transformer3DModel.norm), applied to ``x + add[:, :, None, None]`` when ``add`` ((b f), c) is
+    given, then optionally SiLU (K7).  Under frame sharding the clip-spanning norms merge their
+    statistics over the ranks even when this rank holds a single frame.
     ``x2``: the input is torch.cat([x, x2], dim=1) (an up block's skip concatenation), read from the
     two tensors without materialising the cat."""
     if x2 is not None and autograd.needs_grad(x, x2, norm.weight, norm.bias, add):
@@ -60,7 +70,7 @@ def group_norm_frames(x: torch.Tensor, norm: nn.GroupNorm, frames: int, silu: bo
         x = x.contiguous(memory_format=torch.channels_last)
     if x2 is not None and not x2.is_contiguous(memory_format=torch.channels_last):
         x2 = x2.contiguous(memory_format=torch.channels_last)
-    shard = frame_parallel.active() if frames > 1 else None
+    shard = clip_shard(per_frame)
     w, b = (norm.weight, norm.bias) if norm.affine else (None, None)
     add = None if add is None else add.contiguous()
     if autograd.needs_grad(x, w, b, add):
@@ -208,14 +218,14 @@ class ResnetBlock3D(nn.Module):
             h, stats = fused
             n2 = self.norm2
             h = ops.group_norm_from_partials(h, n2.num_groups, n2.weight, n2.bias, n2.eps, frames, stats, silu=True,
-                                             shard=frame_parallel.active() if frames > 1 else None)
+                                             shard=clip_shard())
         else:
             h = self.conv1(hn)
             h = self.dropout(group_norm_frames(h, self.norm2, frames, silu=True, add=t))
         if self.output_scale_factor != 1.0:
             return (sc + self.conv2(h)) / self.output_scale_factor
         nxt = self.__dict__.get("_next_norm")       # the GroupNorm that reads this output next, if known
-        if nxt is not None and self._conv_gn_ok(self.conv2, h, sc) and nxt.affine:
+        if nxt is not None and self._conv_gn_ok(self.conv2, h, sc, residual=True) and nxt.affine:
             r = ops.conv2d_gn(h, self.conv2.weight, self.conv2.bias, 1, 1, None, nxt.num_groups, 1, residual=sc)
             if r is not None:
                 _PENDING_STATS[id(r[0])] = r       # per-frame statistics for Transformer3DModel.norm
@@ -232,15 +242,16 @@ class ResnetBlock3D(nn.Module):
         return self._conv_gn_ok(self.conv1, hn, t)
 
     @staticmethod
-    def _conv_gn_ok(conv, x, extra) -> bool:
-        """A plain 3x3 InflatedConv3d at inference on bf16 that the per-shape table puts on K10."""
+    def _conv_gn_ok(conv, x, extra, residual: bool = False) -> bool:
+        """A plain 3x3 InflatedConv3d at inference on bf16 that the per-shape table puts on K10
+        (looked up under the key of the unfused call: ``residual`` for conv2(h, residual=sc))."""
         if autograd.needs_grad(x, conv.weight, conv.bias, extra):
             return False
         if type(conv) is not InflatedConv3d or conv._forward_hooks or conv._forward_pre_hooks:
             return False
         if x.dtype != torch.bfloat16 or not x.is_cuda or conv.kernel_size != (3, 3) or conv.stride != (1, 1):
             return False
-        return ops.CONV.prefers_k10(x, conv.weight, 1, 1)
+        return ops.CONV.prefers_k10(x, conv.weight, 1, 1, residual=residual)
 
 
 class GEGLU(nn.Module):
@@ -346,7 +357,7 @@ class Transformer3DModel(nn.Module):
             n = self.norm
             h = ops.group_norm_from_partials(x, n.num_groups, n.weight, n.bias, n.eps, 1, st)
         else:
-            h = group_norm_frames(x, self.norm, 1)
+            h = group_norm_frames(x, self.norm, 1, per_frame=True)
         tok = h.permute(0, 2, 3, 1).reshape(Bf, H * W, C)
         tok = ops.linear(tok, self.proj_in.weight.view(self.proj_in.out_channels, -1), self.proj_in.bias)
         for blk in self.transformer_blocks:
