@@ -38,6 +38,8 @@ EDITS = {
     "car2": ("car", 2, 12, (0, 9, 10, 11)),
     "rabbit8": ("rabbit", 8, 50, (0, 10, 11, 24, 25, 49)),
     "penguin24": ("penguin", 24, 12, (10, 11)),
+    # configs[2] past the self-replace boundary (self_replace_steps 0.5 of 50: steps 24 / 25) to step 26
+    "penguin24l": ("penguin", 24, 27, (10, 11, 24, 25, 26)),
 }
 
 

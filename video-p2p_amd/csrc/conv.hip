@@ -45,6 +45,13 @@
 namespace vp2p {
 namespace conv {
 
+// the main loop's fragment reads software-pipelined against the MFMAs (conv_tile; 0: the compiler's
+// order, kept for A/B)
+#ifndef VP2P_K10_PIPE
+#define VP2P_K10_PIPE 1
+#endif
+constexpr bool kPipe = VP2P_K10_PIPE;
+
 constexpr int BN = 160, BK = 64;
 constexpr int CROW = BN + 8;                    // epilogue tile row (elements)
 
@@ -428,6 +435,46 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
     const char* As = smem + cur * Cfg::STAGE;
     const char* Bs = As + Cfg::TBM * Cfg::RB;
     cur = cur + 1 == Cfg::NSTAGE ? 0 : cur + 1;
+    if constexpr (kPipe && Cfg::NSTAGE == 2 && Cfg::CPW == 8 && (AM != 0 || Cfg::NWV <= 4)) {
+      // Fragment reads software-pipelined against the MFMAs, slot by slot.  Per 32-channel k-step
+      // the smaller operand set is held (H: the wave's B fragments when WTN <= WTM, else its A
+      // fragments) and the larger one rotates through three registers (R): group g issues the
+      // NH MFMAs of rotating fragment g and the read of fragment g + 2; the second k-step's held
+      // set is read during the first k-step's groups.  Every read is then >= 2 groups (>= 2 NH
+      // MFMAs) ahead of its first use instead of just before it, and each group is pinned by a
+      // sched_barrier (left to itself hipcc issued the A reads in pairs right before their MFMAs:
+      // s_waitcnt lgkmcnt(1 / 0) every 5 MFMAs).
+      constexpr bool HB = Cfg::WTN <= Cfg::WTM;
+      constexpr int NH = HB ? Cfg::WTN : Cfg::WTM, NR = HB ? Cfg::WTM : Cfg::WTN;
+      auto ldA = [&](int ks, int i) {
+        const int r = wm * Cfg::WR + 16 * i + fr;
+        return *reinterpret_cast<const bf16x8*>(As + r * Cfg::RB + Cfg::swz(r, 4 * ks + fq) * 16);
+      };
+      auto ldB = [&](int ks, int j) {
+        const int r = wn * Cfg::WN + 16 * j + fr;
+        return *reinterpret_cast<const bf16x8*>(Bs + r * Cfg::RB + Cfg::swz(r, 4 * ks + fq) * 16);
+      };
+      auto ldH = [&](int ks, int k) { return HB ? ldB(ks, k) : ldA(ks, k); };
+      auto ldR = [&](int ks, int k) { return HB ? ldA(ks, k) : ldB(ks, k); };
+      bf16x8 H[2][NH], R[3];
+#pragma unroll
+      for (int k = 0; k < NH; ++k) H[0][k] = ldH(0, k);
+      R[0] = ldR(0, 0);
+      R[1] = ldR(0, 1);
+#pragma unroll
+      for (int g = 0; g < 2 * NR; ++g) {
+        const int ks = g / NR, rr = g - ks * NR, gn = g + 2;
+        if (gn < 2 * NR) R[gn % 3] = ldR(gn / NR, gn % NR);
+        if (ks == 0 && rr < NH) H[1][rr] = ldH(1, rr);
+#pragma unroll
+        for (int k = 0; k < NH; ++k) {
+          if constexpr (HB) acc[rr][k] = mfma16(R[g % 3], H[ks][k], acc[rr][k]);
+          else acc[k][rr] = mfma16(H[ks][k], R[g % 3], acc[k][rr]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
+    }
 #pragma unroll
     for (int ks = 0; ks < Cfg::CPW; ks += 4) {   // chunk index of the 32-channel MFMA k-step (0 or 4)
       bf16x8 af[Cfg::WTM], bfr[Cfg::WTN];
