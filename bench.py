@@ -95,8 +95,9 @@ def parse():
                     help="1 (default): in-tree tuned MIOpen database (vp2p.tuning); 0: library heuristics")
     ap.add_argument("--inner-steps", type=int, default=10, help="null-text Adam iterations per DDIM step")
     ap.add_argument("--shard", default="frames", choices=["frames", "clips"],
-                    help="frames (default): one clip over all ranks (CFG split x frame sharding, strong "
-                         "scaling); clips: every rank edits its own clip (weak scaling, no collective)")
+                    help="frames (default): one clip over all ranks (CFG split x frame sharding; --scale picks "
+                         "whether the headline clip grows with N); clips: every rank edits its own clip (no "
+                         "collective)")
     return ap.parse_args()
 
 
@@ -700,6 +701,22 @@ def main():
                                        "attn_mfma_util_fp32": None if a32 is None else a32["mfma_util"],
                                        "output_finite": bool(torch.isfinite(out32).all().item())}
                 del e32
+        if extras and (world == 1 or frames_mode):
+            # secondary: configs[2] -- the penguin-run refine edit (seq_aligner mapper + LocalBlend +
+            # Reweight), 24 frames, ONE clip frame-sharded over the N ranks (CFG split x frame shards):
+            # strong scaling where the north star measures it; at N = 1 the single-GPU point of that curve
+            edit = None
+            torch.cuda.empty_cache()
+            p_args = argparse.Namespace(**{**vars(args), "frames": 24, "edit": "penguin"})
+            p_lay = EditLayout() if world > 1 else None
+            peng = Edit(p_args, dev, dtype, p_lay, seed_offset=0)
+            t_p, _ = _time_edits(peng, 1, 1, world, dev)
+            result["strong_scaling_24f"] = {
+                "value": round(24 / t_p, 4), "unit": "edited frames/s", "ms_per_step": round(t_p * 1e3, 2),
+                "frames": 24, "scaling": "strong", "config": "configs[2]: " + peng.name + " --fast, " + peng.kind,
+                "parallelism": (p_lay.describe() + " (RCCL)") if p_lay is not None else "single GPU"}
+            del peng
+            torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(f, args.ddim_steps)

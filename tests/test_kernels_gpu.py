@@ -53,13 +53,13 @@ def _prescale(q, d):
 @pytest.mark.parametrize("prescaled", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("d,frames,n", [(40, 3, 200), (80, 2, 256), (160, 2, 144), (40, 8, 64), (40, 2, 300),
-                                         (40, 2, 128), (40, 2, 256)])
+                                         (40, 2, 128), (40, 2, 256), (80, 3, 200), (160, 2, 256), (160, 3, 64)])
 def test_frame_attention(dtype, d, frames, n, prescaled):
     """Both query conventions: plain q (scale applied in the kernel) and q pre-multiplied by
     scale*log2(e) (the production call, FrameAttention.forward; at d = 40 bf16 it selects the
     folded-max kernel, whose ragged 128-key tiles n = 200 / 64 / 300 exercise; n = 256, a multiple
     of the pp kernel's 256-key tile, takes the res-64 pp kernel as a single tile, n = 128 the x2f
-    kernel: several pp tiles are test_frame_attention_pp_tiles)."""
+    kernel: several pp tiles are test_frame_attention_pp_tiles; d = 80 / 160: x2f / one-set)."""
     from vp2p import ops
     heads, B = 8, 2
     C = heads * d
@@ -81,15 +81,19 @@ def test_frame_attention(dtype, d, frames, n, prescaled):
     assert torch.equal(out0, out)
 
 
-@pytest.mark.parametrize("n,spikes", [(1024, (300, 900)), (4096, (300, 1380)), (4096, ())])
-def test_frame_attention_pp_tiles(n, spikes):
-    """The res-64 pp kernel (bf16, d = 40, pre-scaled q, 256-key tiles) over 4 and 16 tiles: its
-    3-slot LDS ring wraps (tile t + 2 lands in tile t - 1's slot) and its XOR-swizzled image is read
-    at every block offset.  Spike keys in tile 1 and in tile 3 / 5 make the row-sum growth check
-    move m part-way through the key axis, rescaling the in-flight P and S (the check runs after
-    every second tile).  float64 oracle on the same bf16 inputs, 2e-2 of max|ref|, plus the lse."""
+@pytest.mark.parametrize("d,n,spikes", [(40, 1024, (300, 900)), (40, 4096, (300, 1380)), (40, 4096, ()),
+                                         (80, 1024, (300, 700)), (80, 2048, (200, 1500)), (80, 128, ()),
+                                         (160, 256, (70, 200)), (160, 1024, (100, 700)), (160, 64, (20,))])
+def test_frame_attention_pp_tiles(d, n, spikes):
+    """The UNet's bf16 pre-scaled call over many key tiles: d = 40 is the pipelined kernel
+    (frame_attn_pp.hip, 256-key tiles: 4 and 16 tiles, its 3-slot LDS ring wraps -- tile t + 2 lands
+    in tile t - 1's slot -- and its XOR-swizzled image is read at every block offset); d = 80 / 160
+    the x2f / one-set kernels at the res-32 / res-16 / res-8 key counts and beyond.  Spike keys in an
+    early and a later tile make the running max move part-way through the key axis (the pp kernel's
+    row-sum growth check every 512 keys rescales its in-flight P and S).  float64 oracle on the same
+    bf16 inputs, 2e-2 of max|ref|, plus the lse."""
     from vp2p import ops
-    heads, B, frames, d = 2, 1, 2, 40
+    heads, B, frames = 2, 1, 2
     C = heads * d
     q = _rand((B * frames, n, C), 11, 1.0)
     k = _rand((B, n, C), 12, 1.0)
@@ -127,17 +131,19 @@ def test_frame_attention_large_logits():
     assert _rel(_np(out), ref) < 1e-4
 
 
+@pytest.mark.parametrize("d", [40, 80, 160])
 @pytest.mark.parametrize("prescaled", [False, True])
 @pytest.mark.parametrize("spike", [4.0, 12.0, "overflow", "overflow_v"])
-def test_frame_attention_bf16_spikes(spike, prescaled):
-    """bf16 d=40 (the x2f kernel): a late key whose logits jump far above the first block's max.
+def test_frame_attention_bf16_spikes(spike, prescaled, d):
+    """bf16 (d = 40: the x2f kernel; d = 80: x2f; d = 160: one-set): a late key whose logits jump far
+    above the first block's max.
     4x / 12x exercise the row-sum rescale; "overflow" aligns the key with one query so that its logit
     is ~100 nats above the running max (p would overflow bf16/fp32), forcing the exact per-row
     fallback; "overflow_v" puts the logit ~80 nats up (p ~ 2^114, the row sum stays finite) on a
     value row of magnitude 2^20, so only the O accumulator overflows -- the fallback must catch that
     too.  Tolerance: the bf16 bar of the north star, 2e-2 of max|ref|."""
     from vp2p import ops
-    heads, B, frames, n, d = 8, 1, 2, 512, 40
+    heads, B, frames, n = 8, 1, 2, 512
     C = heads * d
     q = _rand((B * frames, n, C), 4, 1.0)
     k = _rand((B * frames, n, C), 5, 1.0)

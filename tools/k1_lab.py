@@ -1,5 +1,5 @@
 """K1 A/B over lab builds: each library in argv runs in its own child process (VP2P_LIB) and times
-the res-64 (d 40, pre-scaled q: the UNet's call) and res-32 (d 80) FrameAttention launches of the
+the res-64 (d 40, pre-scaled q: the UNet's call), res-32 (d 80), res-16 and res-8 (d 160) FrameAttention launches of the
 edit (B=4, f=8) with HIP events, checking a slice against a float64 softmax(QK^T)V.
 usage: python tools/k1_lab.py OUT.jsonl lib1.so [lib2.so ...]   (rounds alternate the libraries)"""
 import json
@@ -14,7 +14,7 @@ from vp2p import ops
 B, f, heads = 4, 8, 8
 g = torch.Generator(device="cuda").manual_seed(0)
 rows = []
-for hw, C in ((4096, 320), (1024, 640)):
+for hw, C in ((4096, 320), (1024, 640), (256, 1280), (64, 1280)):
     d = C // heads
     c = ops.frame_query_scale(d)
     q = torch.randn(B * f, hw, C, device="cuda", dtype=torch.bfloat16, generator=g)
@@ -22,7 +22,7 @@ for hw, C in ((4096, 320), (1024, 640)):
     v0 = torch.randn(B, hw, C, device="cuda", dtype=torch.bfloat16, generator=g)
     qq = (q.double() * c).bfloat16()
     o = ops.frame_attention(qq, k0, v0, f, heads, q_prescaled=True)
-    bi, fi, nq = 1, 5, 512
+    bi, fi, nq = 1, 5, min(512, hw)
     qs = qq[bi * f + fi, :nq].double().view(nq, heads, d).transpose(0, 1)
     ks = k0[bi].double().view(hw, heads, d).transpose(0, 1)
     vs = v0[bi].double().view(hw, heads, d).transpose(0, 1)
