@@ -32,7 +32,8 @@ def main():
     plan = ctrl.plan("cuda")
     B, f, heads = 4, 8, 8
     cases = [("res64_edit", 4096, 320, 3, False), ("res64_noedit", 4096, 320, 30, False),
-             ("res32_edit", 1024, 640, 3, False), ("res16_lb", 256, 1280, 30, True)]
+             ("res32_edit", 1024, 640, 3, False), ("res16_lb", 256, 1280, 30, True),
+             ("res16_edit_lb", 256, 1280, 3, True)]
     for name, hw, C, step, lb in cases:
         g = torch.Generator(device="cuda").manual_seed(0)
         q = torch.randn(B * f, hw, C, device="cuda", dtype=torch.bfloat16, generator=g)

@@ -620,15 +620,20 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
 // the word-alpha blend exactly as cross_attn_kernel (v1) does; Q is prefetched one (block, prompt)
 // ahead.  Replaces v1 on these rows (v1: K/V re-read from L2 per item, one item per workgroup).
 // ------------------------------------------------------------------------------------------------
+template <int D> constexpr int v3e_threads() { return D <= 80 ? 512 : 128; }
 template <int D, int KB>
 struct CrossV3eCfg {
   using V3 = CrossV3Cfg<D, KB>;
-  static constexpr int NW = 8;                                   // waves (query streams)
+  // waves (query streams): d 160's two prompts' K / V^T take 132 KB of LDS, leaving room for the
+  // parked source probabilities of two streams only (one workgroup per CU, two waves)
+  static constexpr int NW = D <= 80 ? 8 : 2;
+  static constexpr int NT = 64 * NW;
+  static_assert(NT == v3e_threads<D>(), "launch bound");
   static constexpr int KV = 2 * V3::LDS;                         // both prompts' K, V^T
 };
 
 template <int D, int KB, bool T77 = false>
-__global__ __launch_bounds__(512, 1) void cross_attn_kernel_v3e(const vp2p_cross_attn_args a, int iters, int nx, int prow) {
+__global__ __launch_bounds__(v3e_threads<D>(), 1) void cross_attn_kernel_v3e(const vp2p_cross_attn_args a, int iters, int nx, int prow) {
   using T = bf16;
   using M = Mfma<T>;
   using C = CrossCfg<T, D>;
@@ -656,7 +661,7 @@ __global__ __launch_bounds__(512, 1) void cross_attn_kernel_v3e(const vp2p_cross
   const T* ws = static_cast<const T*>(a.kv_ws);
   const int64_t kelems = (int64_t)a.batch * a.heads * KP * C::DP;
   constexpr int KV8 = KP * C::DP / 8, VV8 = C::DV * KP / 8;
-  for (int i = tid; i < 2 * (KV8 + VV8); i += 512) {
+  for (int i = tid; i < 2 * (KV8 + VV8); i += E::NT) {
     const int p = i / (KV8 + VV8), j0 = i - p * (KV8 + VV8);
     const int b = brow0 + p;
     T* Ks = Ks0 + p * (V3::LDS / 2);
@@ -675,7 +680,7 @@ __global__ __launch_bounds__(512, 1) void cross_attn_kernel_v3e(const vp2p_cross
   // term (Refine: P_src[mapper[w]]; Replace: sum_j P_src[j] M[j, w]; otherwise P_src[w]), A = a eq al,
   // B = (1 - a) eq al + (1 - al) (Refine; a = 0 and the (1 - a) term dropped otherwise), al = alpha_t[w],
   // eq the Reweight equalizer (1 without): one gather and one FMA per score instead of the chain
-  for (int i = tid; i < NKV; i += 512) {
+  for (int i = tid; i < NKV; i += E::NT) {
     const bool refine = a.edit_mode == VP2P_EDIT_REFINE;
     const float ra = refine ? a.refine_alpha[i] : 0.f;
     const float eq = a.reweight ? a.equalizer[i] : 1.f;
@@ -688,7 +693,7 @@ __global__ __launch_bounds__(512, 1) void cross_attn_kernel_v3e(const vp2p_cross
     etab[i] = t;
   }
   if (lb)
-    for (int i = tid; i < LBS * 2 * NKV; i += 512) lbw[i] = a.lb_word_alpha[i];
+    for (int i = tid; i < LBS * 2 * NKV; i += E::NT) lbw[i] = a.lb_word_alpha[i];
   __syncthreads();
 
   const float cs = a.scale * kLog2e;
@@ -949,7 +954,7 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
     if (lds > 160 * 1024) return VP2P_E_SHAPE;
     const int64_t qblocks = (FQ + 31) / 32;
     const int64_t per_wg = (qblocks + E::NW - 1) / E::NW;
-    // ~1 workgroup per CU over the heads; each of its 8 streams then loops `iters` blocks
+    // ~1 workgroup per CU over the heads; each of its NW streams then loops `iters` blocks
     int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (256 + a->heads - 1) / a->heads));
     const int iters = (int)((per_wg + nx - 1) / nx);
     nx = (per_wg + iters - 1) / iters;
@@ -961,9 +966,9 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
     if (!attr || !attr77) return VP2P_E_LAUNCH;
     const dim3 grid((unsigned)(nx * a->heads));
     if (KB == 3 && a->tokens_kv == 77)
-      hipLaunchKernelGGL((cross_attn_kernel_v3e<D, KB, true>), grid, dim3(512), lds, s, *a, iters, (int)nx, prow);
+      hipLaunchKernelGGL((cross_attn_kernel_v3e<D, KB, true>), grid, dim3(E::NT), lds, s, *a, iters, (int)nx, prow);
     else
-      hipLaunchKernelGGL((cross_attn_kernel_v3e<D, KB>), grid, dim3(512), lds, s, *a, iters, (int)nx, prow);
+      hipLaunchKernelGGL((cross_attn_kernel_v3e<D, KB>), grid, dim3(E::NT), lds, s, *a, iters, (int)nx, prow);
     return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
   };
   int g_first = 0;              // first CFG half / batch row the v1 kernel takes
