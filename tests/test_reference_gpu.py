@@ -202,8 +202,8 @@ def _edit_fixture(name):
 
 
 # End-to-end bars: fp32 -- final-latent PSNR >= 100 dB and K6's applied LocalBlend masks
-# equal to the reference's (at most 1 flip per 10^4 pixels); bf16 -- final-latent PSNR >= 45 dB.  Every
-# saved reference mask is non-trivial (true fraction in [0.05, 0.95], asserted by the generator and here;
+# equal to the reference's (at most 1 flip per 10^4 pixels); bf16 -- final-latent PSNR >= 45 dB and at
+# most 2% of the mask pixels flipped.  Every saved reference mask is non-trivial (true fraction in [0.05, 0.95], asserted by the generator and here;
 # the blend maps are summed over steps, so late masks that widen past 0.95 are not saved, only their
 # fraction -- the first blend step's mask always is).
 # The fp32 rabbit8 case runs 50 fp32 UNet steps (~145 s, profiles/r02_edit_pipeline_durations.log),
@@ -236,8 +236,8 @@ def test_edit_vs_reference_pipeline(tokenizer, bench_state, name, dtype, bar):
             assert ((frac >= 0.05) & (frac <= 0.95)).all(), f"vacuous reference mask at step {i}: {frac}"
             flips = int((masks[i] != ref_mask).sum())
             report.append((i, "mask flips", flips, masks[i].size, "ref true frac", [round(float(x), 3) for x in frac]))
-            if dtype == torch.float32:
-                assert flips <= max(1, masks[i].size // 10000), report
+            # fp32: at most 1 flip per 10^4 pixels; bf16: at most 2% (measured 0.1-0.9%, profiles/r04_parity.jsonl)
+            assert flips <= (max(1, masks[i].size // 10000) if dtype == torch.float32 else masks[i].size // 50), report
     assert n_masks > 0, "fixture holds no LocalBlend mask"
     record(f"edit/{name}/{dtype}", steps=report, final_psnr=psnr(lats[save[-1]], gold[f"latents/{save[-1]}"]),
            bar=bar)
