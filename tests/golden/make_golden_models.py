@@ -24,10 +24,10 @@ Parts (``--part``, default ``models``):
                 configs (model_spec.NULLTEXT): the 256/512-channel UNet on a 32^2 latent and the
                 SD-1.5 geometry on a 16^2 latent; saves every inner loss, the optimised unconditional
                 embeddings and the inversion latents.  ~2 min.
-  car2 | rabbit8 | penguin24
+  car2 | rabbit8 | penguin24l
              -> golden_edit_<part>.npz: the fast-mode P2P edit of model_spec.EDITS[part] through
                 the reference pipeline loop at the SD-1.5 geometry, 512^2 (64^2 latent).  CPU-hours
-                for rabbit8/penguin24 (run in the background).
+                for rabbit8/penguin24l (run in the background).
 """
 from __future__ import annotations
 

@@ -290,7 +290,8 @@ def test_frame_sharded_nulltext_matches_single(tmp_path):
 def _penguin_worker(rank, world, port, out_path):
     """configs[2] (penguin-run refine edit, 24 frames, SD-1.5 geometry, bf16) under the bench's
     4-rank EditLayout: CFG split x 2 frame shards of 12 frames each (all ranks on the one GPU, gloo
-    with host staging).  The reference fixture's 12 saved steps are what it is compared against."""
+    with host staging).  Run to step 26 of 50, past the self-replace boundary (steps 24 / 25), the
+    steps the reference fixture saved (golden_edit_penguin24l.npz)."""
     dist = _init(rank, world, port)
     import model_spec as MS
     import spec
@@ -299,7 +300,7 @@ def _penguin_worker(rank, world, port, out_path):
     from vp2p.pipeline import VideoP2PPipeline
     from vp2p.tokenizer import SyntheticCLIPTokenizer
     from vp2p.unet3d import UNet3DConditionModel, init_random_
-    edit, f, steps, save = MS.EDITS["penguin24"]
+    edit, f, steps, save = MS.EDITS["penguin24l"]
     prompts, swap, blend, eq, cross, self_ = spec.CONFIGS[edit]
     tok = SyntheticCLIPTokenizer()
     state = init_random_(UNet3DConditionModel(), seed=0).state_dict()
@@ -310,7 +311,7 @@ def _penguin_worker(rank, world, port, out_path):
     ctrl = vp2p.make_controller(prompts, swap, {"default_": cross}, self_, ((blend[0],), (blend[1],)), eq,
                                 tokenizer=tok)
     vp2p.register_attention_control(type("M", (), {"unet": unet})(), ctrl)
-    inp = MS.edit_inputs("penguin24", MS.blend_token_ids(prompts, blend, tok))
+    inp = MS.edit_inputs("penguin24l", MS.blend_token_ids(prompts, blend, tok))
     lay = EditLayout()
     pipe = VideoP2PPipeline(unet)
     pipe.keep_blend_mask = True
@@ -344,20 +345,21 @@ def _penguin_worker(rank, world, port, out_path):
 @pytest.mark.timeout(600)
 def test_sharded_penguin24_vs_reference(tmp_path):
     """SURVEY §8(e) at a real configuration: the 4-rank layout (CFG split x 2 frame shards) of the
-    24-frame penguin refine edit against the reference pipeline's fixture (golden_edit_penguin24.npz,
-    12 of 50 steps).  Bar: the bf16 end-to-end bar, final-latent PSNR >= 45 dB; the LocalBlend mask
-    flips against the reference are reported (bf16: informational, as for the single-rank case)."""
+    24-frame penguin refine edit against the reference pipeline's fixture (golden_edit_penguin24l.npz,
+    27 of 50 steps: latents at 10, 11 and across the self-replace boundary 24 / 25 / 26).  Bar: the
+    bf16 end-to-end bar, final-latent PSNR >= 45 dB, and at most 2 % of the LocalBlend mask pixels
+    flipped against the reference (as for the single-rank case)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import model_spec as MS
     from conftest import record
-    path = os.path.join(ROOT, "tests", "golden", "golden_edit_penguin24.npz")
+    path = os.path.join(ROOT, "tests", "golden", "golden_edit_penguin24l.npz")
     if not os.path.exists(path):
-        pytest.skip("golden_edit_penguin24.npz not generated")
+        pytest.skip("golden_edit_penguin24l.npz not generated")
     gold = np.load(path)
     out = str(tmp_path / "penguin")
     mp.spawn(_penguin_worker, args=(4, _port(), out), nprocs=4, join=True)
-    _, f, steps, save = MS.EDITS["penguin24"]
+    _, f, steps, save = MS.EDITS["penguin24l"]
     for r in range(4):
         got = torch.load(out + f".{r}")
         assert got["cur_step"] == int(gold["cur_step"]) and got["lb_counter"] == int(gold["lb_counter"]), r

@@ -203,18 +203,19 @@ def _edit_fixture(name):
 
 # End-to-end bars: fp32 -- final-latent PSNR >= 100 dB and K6's applied LocalBlend masks
 # equal to the reference's (at most 1 flip per 10^4 pixels); bf16 -- final-latent PSNR >= 45 dB and at
-# most 2% of the mask pixels flipped.  Every saved reference mask is non-trivial (true fraction in [0.05, 0.95], asserted by the generator and here;
-# the blend maps are summed over steps, so late masks that widen past 0.95 are not saved, only their
-# fraction -- the first blend step's mask always is).
+# most 2% of the mask pixels flipped.  Every saved reference mask is non-trivial (true fraction in
+# [0.05, 0.95], asserted by the generator and here; the blend maps are summed over steps, so late masks
+# that widen past 0.95 are not saved, only their fraction -- the first blend step's mask always is).
 # The fp32 rabbit8 case runs 50 fp32 UNet steps (~145 s, profiles/r02_edit_pipeline_durations.log),
 # more than a 120 s per-test limit on the command line allows.
-# penguin24-fp32 (configs[2] at the reference's precision): its fp32 convolutions run on MIOpen (K10 is
-# bf16), whose compiled kernels for the 24-frame shapes come from the in-tree cache (miopen_db/kcache,
-# vp2p.tuning) instead of minutes of compiling on a fresh box.
+# penguin24l (configs[2], 24 frames): 27 of the 50 steps, latents saved at 10 / 11 (the first blend
+# steps) and 24 / 25 / 26 (across the self-replace boundary).  In fp32 (the reference's precision) its
+# convolutions run on MIOpen (K10 is bf16), whose compiled kernels for the 24-frame shapes come from the
+# in-tree cache (miopen_db/kcache, vp2p.tuning) instead of minutes of compiling on a fresh box.
 EDIT_CASES = [pytest.param(n, dt, bar, id=f"{n}-{'fp32' if dt == torch.float32 else 'bf16'}")
               for n, dt, bar in (("car2", torch.float32, 100.0), ("car2", torch.bfloat16, 45.0),
                                  ("rabbit8", torch.float32, 100.0), ("rabbit8", torch.bfloat16, 45.0),
-                                 ("penguin24", torch.float32, 100.0), ("penguin24", torch.bfloat16, 45.0))]
+                                 ("penguin24l", torch.float32, 100.0), ("penguin24l", torch.bfloat16, 45.0))]
 
 
 @pytest.mark.timeout(600)
