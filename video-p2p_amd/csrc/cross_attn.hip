@@ -349,6 +349,34 @@ struct CrossV3Cfg {
   static constexpr int LDS = (KP * KROW + C::DV * VROW) * 2;
 };
 
+// Staging of the prepared K [KP][DP] / V^T [DV][KP] fragments into padded LDS rows.  A segment is N
+// contiguous 16-byte vectors of the workspace whose rows of RV vectors land RS vectors apart in LDS;
+// a thread's vectors are i = tid + j * NT.  All of a thread's loads of the segments it is given go
+// out before its stores (a load-then-store loop waits out one L2 latency per vector), and the
+// addressing is one multiply-high per vector (the per-vector (prompt, K | V, row) decode it replaced
+// was ~60 % of v3e's VALU instructions at d = 160).
+template <int NT, int N, int RV, int RS>
+struct StageSeg {
+  static constexpr int PER = (N + NT - 1) / NT;
+  const u32x4* src;
+  u32x4* dst;
+  u32x4 buf[PER];
+  __device__ __forceinline__ void load(int tid) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * NT;
+      if (N % NT == 0 || i < N) buf[j] = src[i];
+    }
+  }
+  __device__ __forceinline__ void store(int tid) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * NT;
+      if (N % NT == 0 || i < N) dst[i + (i / RV) * (RS - RV)] = buf[j];
+    }
+  }
+};
+
 // T77: the SD text context (77 tokens, KB = 3): in the last 32-key block only keys 64..76 are real,
 // so accumulator registers 8..15 (keys 80..95 for both lane halves) are never computed through exp
 // and the block's second PV k-step (keys 80..95) is skipped.
@@ -402,14 +430,13 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
   const T* kb_base = ws + ((int64_t)(b * a.heads + head) * KP) * C::DP;
   const T* vb_base = ws + kelems + ((int64_t)(b * a.heads + head) * KP) * C::DV;
   constexpr int KV8 = KP * C::DP / 8, VV8 = C::DV * KP / 8;
-  for (int i = tid; i < KV8 + VV8; i += 256) {
-    if (i < KV8) {
-      const int row = i / (C::DP / 8), c = (i - row * (C::DP / 8)) * 8;
-      *reinterpret_cast<u32x4*>(Ks + row * V3::KROW + c) = *reinterpret_cast<const u32x4*>(kb_base + row * C::DP + c);
-    } else {
-      const int j = i - KV8, row = j / (KP / 8), c = (j - row * (KP / 8)) * 8;
-      *reinterpret_cast<u32x4*>(Vs + row * V3::VROW + c) = *reinterpret_cast<const u32x4*>(vb_base + row * KP + c);
-    }
+  {
+    StageSeg<256, KV8, C::DP / 8, V3::KROW / 8> ks{reinterpret_cast<const u32x4*>(kb_base), reinterpret_cast<u32x4*>(Ks)};
+    StageSeg<256, VV8, KP / 8, V3::VROW / 8> vs{reinterpret_cast<const u32x4*>(vb_base), reinterpret_cast<u32x4*>(Vs)};
+    ks.load(tid);
+    vs.load(tid);
+    ks.store(tid);
+    vs.store(tid);
   }
   if (lb)
     for (int i = tid; i < LBS * NKV; i += 256) {
@@ -619,14 +646,23 @@ __global__ __launch_bounds__(256, D <= 64 ? 3 : 2) void cross_attn_kernel_v3(con
 // rows, fp32), then the edited prompt, whose softmax epilogue applies Replace / Refine, Reweight and
 // the word-alpha blend exactly as cross_attn_kernel (v1) does; Q is prefetched one (block, prompt)
 // ahead.  Replaces v1 on these rows (v1: K/V re-read from L2 per item, one item per workgroup).
+// d = 160 (PAIR below): 4 waves, two per query stream, one per prompt.  Round 5, res-16 edit launch
+// (v3 + v3e + LocalBlend reduce, tools/k2_bench.py, profiles/r05_k2_stage_ab.jsonl): 63.1 -> 38.5 us
+// (v3e 52.9 -> 18.0 us: staging addressing 21 us, the prompt pairs 3 us), bit-equal.
 // ------------------------------------------------------------------------------------------------
-template <int D> constexpr int v3e_threads() { return D <= 80 ? 512 : 128; }
+template <int D> constexpr int v3e_threads() { return D <= 80 ? 512 : 256; }
 template <int D, int KB>
 struct CrossV3eCfg {
   using V3 = CrossV3Cfg<D, KB>;
-  // waves (query streams): d 160's two prompts' K / V^T take 132 KB of LDS, leaving room for the
-  // parked source probabilities of two streams only (one workgroup per CU, two waves)
-  static constexpr int NW = D <= 80 ? 8 : 2;
+  // PAIR (d 160): the two prompts of a query block run on two waves at once -- the source wave parks
+  // its probabilities, a workgroup barrier, the edited wave reads them -- instead of one after the
+  // other on one wave.  d 160's two prompts' K / V^T take 132 KB of LDS, so a CU holds one workgroup
+  // and the edit launch (res-16 / res-8: 64 / 16 query blocks per head) is a few waves per CU, each a
+  // long dependent chain: splitting the prompts across waves halves the chain.  d <= 80 launches have
+  // query blocks enough to fill the CU either way and keep one wave per stream (no barrier).
+  static constexpr bool PAIR = D > 80;
+  static constexpr int NW = D <= 80 ? 8 : 4;                      // waves
+  static constexpr int NS = PAIR ? NW / 2 : NW;                   // query streams (parked-row slots)
   static constexpr int NT = 64 * NW;
   static_assert(NT == v3e_threads<D>(), "launch bound");
   static constexpr int KV = 2 * V3::LDS;                         // both prompts' K, V^T
@@ -640,9 +676,12 @@ __global__ __launch_bounds__(v3e_threads<D>(), 1) void cross_attn_kernel_v3e(con
   using V3 = CrossV3Cfg<D, KB>;
   using E = CrossV3eCfg<D, KB>;
   constexpr int KP = V3::KP;
-  constexpr int NW = E::NW;
+  constexpr int NS = E::NS;
+  constexpr bool PAIR = E::PAIR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 31, h = l >> 5;
+  const int sw = PAIR ? w >> 1 : w;                              // this wave's query stream
+  const int role = PAIR ? w & 1 : 0;                             // PAIR: the prompt this wave computes
   const int NKV = a.tokens_kv;
   const int FQ = a.frames * a.tokens_q;
   const int LBS = a.lb_sets == 2 ? 2 : 1;
@@ -653,29 +692,14 @@ __global__ __launch_bounds__(v3e_threads<D>(), 1) void cross_attn_kernel_v3e(con
   const int brow0 = a.cond_only ? 0 : a.prompts;                // batch row of the source prompt
 
   T* Ks0 = reinterpret_cast<T*>(smem);
-  float* psrc = reinterpret_cast<float*>(smem + E::KV) + (w * 32 + r) * prow;
-  f32x4* etab = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + E::KV) + NW * 32 * prow);
+  float* psrc = reinterpret_cast<float*>(smem + E::KV) + (sw * 32 + r) * prow;
+  f32x4* etab = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + E::KV) + NS * 32 * prow);
   float* lbw = reinterpret_cast<float*>(etab + NKV);             // [set][prompt][word]
 
   // stage both prompts' K [KP][DP] and V^T [DV][KP] (padded rows), the edit table and the LB weights
   const T* ws = static_cast<const T*>(a.kv_ws);
   const int64_t kelems = (int64_t)a.batch * a.heads * KP * C::DP;
   constexpr int KV8 = KP * C::DP / 8, VV8 = C::DV * KP / 8;
-  for (int i = tid; i < 2 * (KV8 + VV8); i += E::NT) {
-    const int p = i / (KV8 + VV8), j0 = i - p * (KV8 + VV8);
-    const int b = brow0 + p;
-    T* Ks = Ks0 + p * (V3::LDS / 2);
-    T* Vs = Ks + KP * V3::KROW;
-    if (j0 < KV8) {
-      const T* src = ws + ((int64_t)(b * a.heads + head) * KP) * C::DP;
-      const int row = j0 / (C::DP / 8), c = (j0 - row * (C::DP / 8)) * 8;
-      *reinterpret_cast<u32x4*>(Ks + row * V3::KROW + c) = *reinterpret_cast<const u32x4*>(src + row * C::DP + c);
-    } else {
-      const T* src = ws + kelems + ((int64_t)(b * a.heads + head) * KP) * C::DV;
-      const int j = j0 - KV8, row = j / (KP / 8), c = (j - row * (KP / 8)) * 8;
-      *reinterpret_cast<u32x4*>(Vs + row * V3::VROW + c) = *reinterpret_cast<const u32x4*>(src + row * KP + c);
-    }
-  }
   // the edit of run_videop2p.py:304-317 folded per word into new = G * A + P_edit * B: G the source
   // term (Refine: P_src[mapper[w]]; Replace: sum_j P_src[j] M[j, w]; otherwise P_src[w]), A = a eq al,
   // B = (1 - a) eq al + (1 - al) (Refine; a = 0 and the (1 - a) term dropped otherwise), al = alpha_t[w],
@@ -694,11 +718,10 @@ __global__ __launch_bounds__(v3e_threads<D>(), 1) void cross_attn_kernel_v3e(con
   }
   if (lb)
     for (int i = tid; i < LBS * 2 * NKV; i += E::NT) lbw[i] = a.lb_word_alpha[i];
-  __syncthreads();
 
   const float cs = a.scale * kLog2e;
-  const int qb0 = bx * NW * iters + w;
-  constexpr int step = 32 * NW;
+  const int qb0 = bx * NS * iters + sw;
+  constexpr int step = 32 * NS;
   int qi = qb0 * 32 + r;
   int fr_n = qi / a.tokens_q, pos_n = qi - fr_n * a.tokens_q;
   auto advance = [&](int& f_, int& p_) {
@@ -713,16 +736,36 @@ __global__ __launch_bounds__(v3e_threads<D>(), 1) void cross_attn_kernel_v3e(con
     for (int s = 0; s < C::KS; ++s) dst[s] = ok ? M::row_frag(row, s, h, D) : M::zero();
   };
   bf16x8 qn[C::KS];
-  load_q(qi, fr_n, pos_n, 0, qn);
+  load_q(qi, fr_n, pos_n, role, qn);     // the first Q block in flight during the staging
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int64_t bh = (int64_t)(brow0 + p) * a.heads + head;
+    T* Ks = Ks0 + p * (V3::LDS / 2);
+    StageSeg<E::NT, KV8, C::DP / 8, V3::KROW / 8> ks{reinterpret_cast<const u32x4*>(ws + bh * KP * C::DP),
+                                                       reinterpret_cast<u32x4*>(Ks)};
+    StageSeg<E::NT, VV8, KP / 8, V3::VROW / 8> vs{reinterpret_cast<const u32x4*>(ws + kelems + bh * KP * C::DV),
+                                                    reinterpret_cast<u32x4*>(Ks + KP * V3::KROW)};
+    ks.load(tid);
+    vs.load(tid);
+    ks.store(tid);
+    vs.store(tid);
+  }
+  __syncthreads();
 
   for (int it = 0; it < iters; ++it) {
     const int qcur = qi, fcur = fr_n, pcur = pos_n;
     const bool qv = qcur < FQ;
-    for (int p = 0; p < 2; ++p) {
+    for (int p = role; p < (PAIR ? role + 1 : 2); ++p) {
       bf16x8 qf[C::KS];
 #pragma unroll
       for (int s = 0; s < C::KS; ++s) qf[s] = qn[s];
-      if (p == 0) {
+      if (PAIR) {
+        if (it + 1 < iters) {
+          advance(fr_n, pos_n);
+          qi += step;
+          load_q(qi, fr_n, pos_n, p, qn);
+        }
+      } else if (p == 0) {
         load_q(qcur, fcur, pcur, 1, qn);
       } else if (it + 1 < iters) {
         advance(fr_n, pos_n);
@@ -779,10 +822,14 @@ __global__ __launch_bounds__(v3e_threads<D>(), 1) void cross_attn_kernel_v3e(con
             const int wd = kb * 32 + acc_row(i, h);
             if (wd < NKV) psrc[wd] = sc[kb][i];
           }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      } else {
+        if (!PAIR) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      }
+      if (PAIR) __syncthreads();          // the source wave's rows parked -> the edited wave reads them
+      if (p == 1) {
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
@@ -858,6 +905,7 @@ __global__ __launch_bounds__(v3e_threads<D>(), 1) void cross_attn_kernel_v3e(con
         }
       }
     }
+    if (PAIR && it + 1 < iters) __syncthreads();   // the parked rows are read before they are rewritten
   }
 }
 
@@ -949,12 +997,12 @@ static int launch_cross(const vp2p_cross_attn_args* a, hipStream_t s) {
     using E = CrossV3eCfg<D, KB>;
     const int prow = a->tokens_kv | 1;
     const int sets = a->lb_sets == 2 ? 2 : 1;
-    const size_t lds = (size_t)E::KV + (size_t)E::NW * 32 * prow * 4 + (size_t)a->tokens_kv * 16 +
+    const size_t lds = (size_t)E::KV + (size_t)E::NS * 32 * prow * 4 + (size_t)a->tokens_kv * 16 +
                        (size_t)sets * 2 * a->tokens_kv * 4;
     if (lds > 160 * 1024) return VP2P_E_SHAPE;
     const int64_t qblocks = (FQ + 31) / 32;
-    const int64_t per_wg = (qblocks + E::NW - 1) / E::NW;
-    // ~1 workgroup per CU over the heads; each of its NW streams then loops `iters` blocks
+    const int64_t per_wg = (qblocks + E::NS - 1) / E::NS;
+    // ~1 workgroup per CU over the heads; each of its NS streams then loops `iters` blocks
     int64_t nx = std::max<int64_t>(1, std::min<int64_t>(per_wg, (256 + a->heads - 1) / a->heads));
     const int iters = (int)((per_wg + nx - 1) / nx);
     nx = (per_wg + iters - 1) / iters;
