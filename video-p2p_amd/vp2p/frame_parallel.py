@@ -245,11 +245,17 @@ class FrameShard:
         return x.narrow(dim, self.rank * fl, fl).contiguous()
 
     def gather(self, x: torch.Tensor, dim: int = 2) -> torch.Tensor:
-        """All ranks' frames concatenated along ``dim`` (every rank gets the full clip)."""
+        """All ranks' frames concatenated along ``dim`` (every rank gets the full clip): one
+        all_gather_into_tensor into a rank-major buffer, then one copy into the clip's layout."""
         src = x.detach().cpu().contiguous() if (self.staged and x.is_cuda) else x.contiguous()
-        parts = [torch.empty_like(src) for _ in range(self.world)]
-        dist.all_gather(parts, src, group=self.group)
-        return torch.cat(parts, dim=dim).to(x.device)
+        if self.world == 1:
+            return src.to(x.device)
+        dim = dim % src.dim()
+        buf = torch.empty((self.world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(buf, src, group=self.group)
+        ranks = buf.view((self.world,) + tuple(src.shape))           # (world, *x.shape)
+        out = ranks.movedim(0, dim).reshape(src.shape[:dim] + (self.world * src.shape[dim],) + src.shape[dim + 1:])
+        return out.to(x.device)
 
     def all_gather_flat(self, t: torch.Tensor) -> torch.Tensor:
         """Every rank's copy of the 1-D tensor ``t`` concatenated in rank order (on t's device):
