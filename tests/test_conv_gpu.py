@@ -287,3 +287,36 @@ def test_conv2d_img_add(n, c, h, cout):
         ref = (ops.conv2d(x, w, b, 1, 1).float() + t.float()[:, :, None, None]).to(torch.bfloat16)
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("M,epi", [(131072, "plain"), (131072, "alpha"), (131072, "residual"), (131072, "nobias"),
+                                   (393216, "residual"), (32768, "plain"), (98336, "residual")])
+def test_k10_stream_k320(M, epi):
+    """K10s, the persistent stream for the K = N = 320 projections (M / 32 >= 1024 whole 32-row blocks,
+    the 64x64-latent transformer blocks at 8 and 24 frames): bit-equal to the tiled kernels, which the
+    same rows take in 16384-row chunks (below the stream's threshold), and within bf16 rounding of the
+    fp32 GEMM.  M = 98336 is 3073 blocks: a ragged last round of the persistent grid."""
+    from vp2p import ops
+    g = torch.Generator().manual_seed(21)
+    K = N = 320
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    b = None if epi == "nobias" else (torch.randn(N, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    r = torch.randn(M, N, generator=g).to(torch.bfloat16).to(DEV) if epi == "residual" else None
+    alpha = 0.2281 if epi == "alpha" else 1.0
+
+    def run(xs, rs):
+        if rs is not None:
+            return ops.linear_residual(xs, w, b, rs)
+        return ops.linear_k10(xs, w, b, alpha)
+
+    with torch.no_grad():
+        full = run(x, r)
+        tiled = torch.cat([run(x[i:i + 16384], None if r is None else r[i:i + 16384]) for i in range(0, M, 16384)])
+    torch.cuda.synchronize()
+    assert torch.equal(full, tiled)
+    ref = alpha * F.linear(x[:4096].float(), w.float(), None if b is None else b.float())
+    if r is not None:
+        ref = ref.to(torch.bfloat16).float() + r[:4096].float()
+    err = (full[:4096].float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
