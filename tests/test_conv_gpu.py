@@ -320,3 +320,35 @@ def test_k10_stream_k320(M, epi):
         ref = ref.to(torch.bfloat16).float() + r[:4096].float()
     err = (full[:4096].float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("M,N,geglu", [(131072, 960, False), (131072, 2560, True), (393216, 2560, True),
+                                       (98336, 960, False)])
+def test_k10_stream_k320_groups(M, N, geglu):
+    """K10s over N = 320 NG column groups: attn_temp's q|k|v (N 960) and the GEGLU projection (N 2560,
+    interleaved weights, the GEGLU epilogue; 8 and 24 frames) -- bit-equal to the tiled kernels on
+    16384-row chunks, and within bf16 rounding of the fp32 reference."""
+    from vp2p import ops
+    g = torch.Generator().manual_seed(22)
+    K = 320
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    with torch.no_grad():
+        if geglu:
+            w_il, b_il = ops.geglu_interleave(w, b)
+            run = lambda xs: ops.linear_geglu(xs, w_il, b_il)           # noqa: E731
+        else:
+            run = lambda xs: ops.linear_k10(xs, w, b)                    # noqa: E731
+        full = run(x)
+        tiled = torch.cat([run(x[i:i + 16384]) for i in range(0, M, 16384)])
+    torch.cuda.synchronize()
+    assert torch.equal(full, tiled)
+    h = F.linear(x[:4096].float(), w.float(), b.float())
+    if geglu:
+        v, gt = h.chunk(2, dim=-1)
+        ref = v.to(torch.bfloat16).float() * F.gelu(gt.to(torch.bfloat16).float())
+    else:
+        ref = h
+    err = (full[:4096].float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-2, err

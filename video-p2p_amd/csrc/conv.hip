@@ -669,65 +669,72 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_s(const vp2p_conv_args a) 
 }
 
 // ------------------------------------------------------------------------------------------------
-// K10s: the K = 320, N = 320 1x1 GEMMs of the 64x64-latent transformer blocks (proj_in, to_q, to_out,
-// proj_out, attn_temp's to_out: y = x W^T (+ bias) (* alpha) (+ residual), M = B f 4096 rows) as a
-// persistent stream.  These are HBM-bound (640 B in and 640 B out per row against 205 KFLOP), and the
-// tiled kernels run them at ~2.9 TB/s: each 256 x 320 tile is 5 K-steps between a prologue and an
-// epilogue that nothing overlaps.  Here one workgroup per CU keeps the whole weight in registers
-// (10 waves x 32 output channels x K 320: 80 VGPRs a lane, read once) and streams 32-row blocks of x
-// through a 4-slot LDS ring by LDS-DMA, three blocks in flight, each block's 32 x 320 output staged
-// in LDS and stored as whole rows.  Per output the same 16x16x32 MFMAs in the same K order as the
-// tiled kernels (one per 32 channels, ascending) and the same epilogue roundings: bit-equal.
+// K10s: the K = 320 1x1 GEMMs of the 64x64-latent transformer blocks as a persistent stream --
+// proj_in, to_q, to_out, proj_out, attn_temp's to_out (N = 320: y = x W^T (+ bias) (* alpha)
+// (+ residual)), attn_temp's q|k|v (N = 960) and the GEGLU projection (N = 2560 interleaved, the
+// GEGLU epilogue); M = B f 4096 rows.  The N = 320 ones are HBM-bound (640 B in and 640 B out per
+// row against 205 KFLOP), and the tiled kernels ran them at ~2.9 TB/s: each 256 x 320 tile is 5
+// K-steps between a prologue and an epilogue that nothing overlaps.  Here a workgroup per CU keeps
+// one 320-column group of W in registers (10 waves x 32 output columns x K 320: 80 VGPRs a lane,
+// read once) and streams 32-row blocks of x through a 4-slot LDS ring by LDS-DMA, three blocks in
+// flight, each block's output staged in LDS and stored as whole row segments.  N = 320 NG: NG
+// workgroups share each row block (consecutive logical ids, so one XCD and its L2), each with its
+// column group.  Per output the same 16x16x32 MFMAs in the same K order as the tiled kernels (one per
+// 32 channels, ascending) and the same epilogue roundings: bit-equal.
 // ------------------------------------------------------------------------------------------------
 #ifndef VP2P_K10_SKINNY
 #define VP2P_K10_SKINNY 1
 #endif
-#ifndef VP2P_K10S_PF          // lab: A fragments read one k-step ahead
-#define VP2P_K10S_PF 0
-#endif
 constexpr int SK_K = 320, SK_N = 320, SK_R = 32, SK_NW = 10, SK_NT = 64 * SK_NW;
 constexpr int SK_BLK = SK_R * SK_K * 2;                            // one block of x rows: 20 KB
-constexpr int SK_OROW = SK_N + 8;                                  // output tile row (elements)
 constexpr int SK_CH = SK_K * 2 / 16;                               // 16-byte chunks per row: 40
-constexpr int SK_EPI = SK_R * (SK_N / 8) / SK_NT;                  // output chunks per thread: 2
-static_assert(SK_R * SK_CH == 2 * 64 * SK_NW && SK_R * (SK_N / 8) == SK_EPI * SK_NT, "one block = 2 DMA per wave");
+static_assert(SK_R * SK_CH == 2 * 64 * SK_NW, "one block = 2 DMA per wave");
 // ring slots: x (and, with a residual, the residual's rows too, also by LDS-DMA: a register load of
-// it would be the youngest vector-memory operation, and waiting for it drains the x prefetch)
+// it would be the youngest vector-memory operation, and waiting for it drains the x prefetch).
 // Without a residual the output tile is double-buffered and block li's rows are stored after the
-// NEXT iteration's barrier: one barrier per block (with one: 101 -> 122 KB of LDS; the residual
-// variant's ring leaves no room for a second tile and keeps a barrier before its stores).
-template <bool RES> struct SkCfg {
+// NEXT iteration's barrier: one barrier per block; the residual variant's ring leaves no room for a
+// second tile and keeps a barrier before its stores.  EPI 1 (GEGLU): a wave's 32 columns are 16
+// value and the 16 matching gate rows of the interleaved weight, its 16 output channels' value and
+// gate in the same lanes; a group writes 160 output channels.
+template <bool RES, int EPI> struct SkCfg {
   static constexpr int ST = RES ? 3 : 4;                         // slots: ST - 1 blocks in flight
   static constexpr int SLOT = (RES ? 2 : 1) * SK_BLK;
   static constexpr int OB = RES ? 1 : 2;                         // output tiles
-  static constexpr int LDS = ST * SLOT + OB * SK_R * SK_OROW * 2;
+  static constexpr int ON = EPI == 1 ? SK_N / 2 : SK_N;          // output columns per group
+  static constexpr int OROW = ON + 8;                            // output tile row (elements)
+  static constexpr int EPC = SK_R * (ON / 8) / SK_NT;            // output chunks per thread per block
+  static constexpr int LDS = ST * SLOT + OB * SK_R * OROW * 2;
   static constexpr int D = RES ? 4 : 2;                          // DMA instructions per wave per block
+  static_assert(SK_R * (ON / 8) == EPC * SK_NT, "whole chunks per thread");
 };
 
-template <bool RES>
+template <bool RES, int EPI>
 __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_args a) {
-  using S = SkCfg<RES>;
+  using S = SkCfg<RES, EPI>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = l & 15, fq = l >> 4;
   const int nblk = a.batch * a.out_h * a.out_w / SK_R;
-  const int G = gridDim.x, g = xcd_remap(blockIdx.x, G);
+  const int NG = a.cout / SK_N;                                    // column groups
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int cg = lid % NG, g = lid / NG, G = gridDim.x / NG;       // group, row-stream index, streams
   const int nmine = g < nblk ? (nblk - g + G - 1) / G : 0;
   bf16* Os = reinterpret_cast<bf16*>(smem + S::ST * S::SLOT);
+  const int ncol = cg * SK_N;                                      // this group's first weight row
 
-  // this wave's 32 output channels: all of W's K for them, as 16x16x32 B fragments (weight row
-  // 32 w + 16 t + fr, channels 32 s + 8 fq .. + 7)
+  // this wave's 32 weight rows: all of K for them, as 16x16x32 B fragments (row ncol + 32 w + 16 t + fr,
+  // channels 32 s + 8 fq .. + 7)
   const bf16* wt = static_cast<const bf16*>(a.w);
   bf16x8 wf[2][SK_K / 32];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int s = 0; s < SK_K / 32; ++s)
-      wf[t][s] = *reinterpret_cast<const bf16x8*>(wt + (int64_t)(32 * w + 16 * t + fr) * SK_K + 32 * s + 8 * fq);
+      wf[t][s] = *reinterpret_cast<const bf16x8*>(wt + (int64_t)(ncol + 32 * w + 16 * t + fr) * SK_K + 32 * s + 8 * fq);
   const bf16* bias = static_cast<const bf16*>(a.bias);
   float bv[2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) bv[t] = bias ? (float)bias[32 * w + 16 * t + fr] : 0.f;
+  for (int t = 0; t < 2; ++t) bv[t] = bias ? (float)bias[ncol + 32 * w + 16 * t + fr] : 0.f;
   const float al = a.alpha == 0.f ? 1.f : a.alpha;
 
   // LDS-DMA: the block's 1280 16-byte slots, slot q = row * 40 + j holding chunk j ^ ((row >> 1) & 7)
@@ -758,35 +765,38 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
                                                  base + ((2 * w + k) * 64 + l) * 16, 0, 0, 0);
   };
   // the in-order vmcnt that retires this wave's DMA of block li counts everything issued after it; in
-  // the steady state: for each of the next ST - 2 iterations its DMA and its SK_EPI stores (and, with
-  // the residual's barrier before the stores, the stores of the iteration that issued it).  The first
+  // the steady state: for each of the next ST - 2 iterations its DMA and its EPC stores (and, with the
+  // residual's barrier before the stores, the stores of the iteration that issued it).  The first
   // ST - 1 blocks and the tail wait for all.
-  constexpr int kYoung = (RES ? SK_EPI : 0) + (S::ST - 2) * (S::D + SK_EPI);
-  static_assert(kYoung == 8, "the immediate below");
+  constexpr int kYoung = (RES ? S::EPC : 0) + (S::ST - 2) * (S::D + S::EPC);
+  static_assert(kYoung == 8 || kYoung == 6, "the immediates below");
 #pragma unroll
   for (int p = 0; p < S::ST - 1; ++p)
     if (p < nmine) dma(p);
 
   bf16* y = static_cast<bf16*>(a.y);
+  const int ystride = EPI == 1 ? a.cout / 2 : a.cout;
+  const int ycol = cg * S::ON;
   // block lj's rows from output tile ob (+ its residual from ring slot sl) as whole 16-byte chunks
   auto store = [&](int lj, int ob, const char* sl) {
-    const bf16* O = Os + ob * SK_R * SK_OROW;
+    const bf16* O = Os + ob * SK_R * S::OROW;
     const int64_t r0 = (int64_t)(g + lj * G) * SK_R;
 #pragma unroll
-    for (int k = 0; k < SK_EPI; ++k) {
-      const int c = tid + k * SK_NT, row = c / (SK_N / 8), ch = c - row * (SK_N / 8);
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(O + row * SK_OROW + ch * 8);
+    for (int k = 0; k < S::EPC; ++k) {
+      const int c = tid + k * SK_NT, row = c / (S::ON / 8), ch = c - row * (S::ON / 8);
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(O + row * S::OROW + ch * 8);
       if constexpr (RES) {
         const bf16x8 rv = *reinterpret_cast<const bf16x8*>(sl + SK_BLK + c * 16);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)rv[j]);
       }
-      *reinterpret_cast<bf16x8*>(y + (r0 + row) * SK_N + ch * 8) = v;
+      *reinterpret_cast<bf16x8*>(y + (r0 + row) * ystride + ycol + ch * 8) = v;
     }
   };
   for (int li = 0; li < nmine; ++li) {
     if (li >= S::ST - 1 && li + S::ST - 2 < nmine) {             // wave-uniform
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if constexpr (kYoung == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -801,51 +811,51 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[i][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    auto lda = [&](int s_, int i) {
-      const int row = 16 * i + fr;
-      return *reinterpret_cast<const bf16x8*>(st + row * SK_K * 2 + ((4 * s_ + fq) ^ ((row >> 1) & 7)) * 16);
-    };
-#if VP2P_K10S_PF
-    bf16x8 af[2][2];                                               // k-step s's fragments and s + 1's
-    af[0][0] = lda(0, 0);
-    af[0][1] = lda(0, 1);
 #pragma unroll
     for (int s = 0; s < SK_K / 32; ++s) {
-      if (s + 1 < SK_K / 32) {
-        af[(s + 1) & 1][0] = lda(s + 1, 0);
-        af[(s + 1) & 1][1] = lda(s + 1, 1);
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = 16 * i + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(st + row * SK_K * 2 + ((4 * s + fq) ^ ((row >> 1) & 7)) * 16);
       }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        acc[0][t] = mfma16(af[0], wf[t][s], acc[0][t]);
+        acc[1][t] = mfma16(af[1], wf[t][s], acc[1][t]);
+      }
+    }
+    bf16* O = Os + (S::OB == 2 ? (li & 1) : 0) * SK_R * S::OROW;
+    if constexpr (EPI == 1) {
+      // the tiled kernels' GEGLU epilogue: value and gate rounded to bf16, gelu rounded, the product
+      // rounded (K9's order)
+#pragma clang fp contract(off)
+      constexpr float kAlpha = 0.70710678118654752440f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4v val = round_bf16x4(acc[i][0] + bv[0]);
+        const f32x4v gt = round_bf16x4(acc[i][1] + bv[1]);
+        const f32x4v ge = round_bf16x4(gt * 0.5f * (1.f + erf_fast4(gt * kAlpha)));
+        const f32x4v o = val * ge;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) O[(16 * i + 4 * fq + e) * S::OROW + 16 * w + fr] = (bf16)o[e];
+      }
+    } else {
+      // the tiled kernels' epilogue roundings: (acc + bias) * alpha -> bf16, then + residual -> bf16
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) acc[i][t] = mfma16(af[s & 1][i], wf[t][s], acc[i][t]);
+        for (int t = 0; t < 2; ++t) {
+          const f32x4v v = (acc[i][t] + bv[t]) * al;
+          const bf16x2v lo = __builtin_convertvector(f32x2v{v[0], v[1]}, bf16x2v);
+          const bf16x2v hi = __builtin_convertvector(f32x2v{v[2], v[3]}, bf16x2v);
+          bf16* c = O + (16 * i + 4 * fq) * S::OROW + 32 * w + 16 * t + fr;
+          c[0] = lo.x;
+          c[S::OROW] = lo.y;
+          c[2 * S::OROW] = hi.x;
+          c[3 * S::OROW] = hi.y;
+        }
     }
-#else
-#pragma unroll
-    for (int s = 0; s < SK_K / 32; ++s) {
-      const bf16x8 a0 = lda(s, 0), a1 = lda(s, 1);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        acc[0][t] = mfma16(a0, wf[t][s], acc[0][t]);
-        acc[1][t] = mfma16(a1, wf[t][s], acc[1][t]);
-      }
-    }
-#endif
-    // the tiled kernels' epilogue roundings: (acc + bias) * alpha -> bf16, then + residual -> bf16
-    bf16* O = Os + (S::OB == 2 ? (li & 1) : 0) * SK_R * SK_OROW;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const f32x4v v = (acc[i][t] + bv[t]) * al;
-        const bf16x2v lo = __builtin_convertvector(f32x2v{v[0], v[1]}, bf16x2v);
-        const bf16x2v hi = __builtin_convertvector(f32x2v{v[2], v[3]}, bf16x2v);
-        bf16* c = O + (16 * i + 4 * fq) * SK_OROW + 32 * w + 16 * t + fr;
-        c[0] = lo.x;
-        c[SK_OROW] = lo.y;
-        c[2 * SK_OROW] = hi.x;
-        c[3 * SK_OROW] = hi.y;
-      }
     if constexpr (RES) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -861,12 +871,23 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
   }
 }
 
-// the K10s shapes: a plain 1x1 GEMM K = N = 320 (bias / alpha / residual epilogues) on whole 32-row
-// blocks, enough of them to give every CU a stream
+template <bool RES, int EPI>
+static int launch_k320(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
+  constexpr int lds = SkCfg<RES, EPI>::LDS;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_k320<RES, EPI>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  if (!attr) return VP2P_E_LAUNCH;
+  hipLaunchKernelGGL((conv_kernel_k320<RES, EPI>), grid, dim3(SK_NT), lds, s, a);
+  return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+}
+
+// the K10s shapes: a 1x1 GEMM with K = 320 and N = 320 NG (NG <= 8; a residual only at N = 320; the
+// plain or the GEGLU epilogue) on whole 32-row blocks, enough of them to give every CU a stream
 static bool skinny_ok(const vp2p_conv_args* a, int64_t M) {
-  return VP2P_K10_SKINNY && a->kernel == 1 && a->stride == 1 && a->cin == SK_K && a->cout == SK_N && !a->x2 &&
-         !a->cin2 && !a->upsample && a->epilogue == VP2P_CONV_EPI_NONE && !a->gn_partials && !a->img_add &&
-         M % SK_R == 0 && M / SK_R >= 1024 && M * SK_K * 2 < ((int64_t)1 << 31);  // 32-bit buffer offsets
+  return VP2P_K10_SKINNY && a->kernel == 1 && a->stride == 1 && a->cin == SK_K && a->cout % SK_N == 0 &&
+         a->cout <= 8 * SK_N && (!a->residual || a->cout == SK_N) && !a->x2 && !a->cin2 && !a->upsample &&
+         (a->epilogue == VP2P_CONV_EPI_NONE || a->epilogue == VP2P_CONV_EPI_GEGLU) && !a->gn_partials &&
+         !a->img_add && M % SK_R == 0 && M / SK_R >= 1024 && M * SK_K * 2 < ((int64_t)1 << 31);  // 32-bit offsets
 }
 
 template <int KS, int EPI, int AM, int CF> struct ConvKernel;
@@ -1092,31 +1113,21 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   const dim3 grid((unsigned)(tiles * k));
   int rc;
   if (conv::skinny_ok(a, M)) {
-    static const bool attr0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_k320<false>),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  conv::SkCfg<false>::LDS) == hipSuccess;
-    static const bool attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv::conv_kernel_k320<true>),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  conv::SkCfg<true>::LDS) == hipSuccess;
-    if (!attr0 || !attr1) return VP2P_E_LAUNCH;
-    int cus = 256;
-    {
-      static int n_cu = 0;
-      if (!n_cu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-          n_cu = 256;
-      }
-      cus = n_cu;
+    const int ng = a->cout / conv::SK_N;
+    static int n_cu = 0;
+    if (!n_cu) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+        n_cu = 256;
     }
     const int64_t nblk = M / conv::SK_R;
-    const dim3 gk((unsigned)(nblk < cus ? nblk : cus));
-    if (a->residual)
-      hipLaunchKernelGGL(conv::conv_kernel_k320<true>, gk, dim3(conv::SK_NT), conv::SkCfg<true>::LDS, s, *a);
-    else
-      hipLaunchKernelGGL(conv::conv_kernel_k320<false>, gk, dim3(conv::SK_NT), conv::SkCfg<false>::LDS, s, *a);
-    rc = hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
+    int64_t streams = n_cu / ng > 0 ? n_cu / ng : 1;               // row streams per column group
+    if (streams > nblk) streams = nblk;
+    const dim3 gk((unsigned)(streams * ng));
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_k320<false, 1>(*a, gk, s);
+    else if (a->residual) rc = conv::launch_k320<true, 0>(*a, gk, s);
+    else rc = conv::launch_k320<false, 0>(*a, gk, s);
   } else if (k > 1) {
     vp2p_conv_args b = *a;
     b.ksplit = k;
