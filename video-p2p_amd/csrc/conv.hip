@@ -685,10 +685,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_s(const vp2p_conv_args a) 
 #ifndef VP2P_K10_SKINNY
 #define VP2P_K10_SKINNY 1
 #endif
-constexpr int SK_K = 320, SK_N = 320, SK_R = 32, SK_NW = 10, SK_NT = 64 * SK_NW;
-constexpr int SK_BLK = SK_R * SK_K * 2;                            // one block of x rows: 20 KB
-constexpr int SK_CH = SK_K * 2 / 16;                               // 16-byte chunks per row: 40
-static_assert(SK_R * SK_CH == 2 * 64 * SK_NW, "one block = 2 DMA per wave");
+constexpr int SK_R = 32, SK_NW = 10, SK_NT = 64 * SK_NW;
 // ring slots: x (and, with a residual, the residual's rows too, also by LDS-DMA: a register load of
 // it would be the youngest vector-memory operation, and waiting for it drains the x prefetch).
 // Without a residual the output tile is double-buffered and block li's rows are stored after the
@@ -696,80 +693,100 @@ static_assert(SK_R * SK_CH == 2 * 64 * SK_NW, "one block = 2 DMA per wave");
 // second tile and keeps a barrier before its stores.  EPI 1 (GEGLU): a wave's 32 columns are 16
 // value and the 16 matching gate rows of the interleaved weight, its 16 output channels' value and
 // gate in the same lanes; a group writes 160 output channels.
-template <bool RES, int EPI> struct SkCfg {
-  static constexpr int ST = RES ? 3 : 4;                         // slots: ST - 1 blocks in flight
-  static constexpr int SLOT = (RES ? 2 : 1) * SK_BLK;
+// KK = 640 (the 32x32-latent projections, W 640 x 640): 16 weight rows a wave (the same 80 VGPRs),
+// 160-column groups, 40 KB blocks in a 3-slot ring; a wave's A fragments then feed one 16-column
+// tile each, so that stream is bound by LDS reads at half the MFMA rate (measured level with the
+// tiled kernels; not dispatched, see skinny_kind).
+template <int KK, int CW, bool RES, int EPI> struct SkCfg {
+  static constexpr int CT = CW / 16;                             // 16-column MFMA tiles per wave
+  static constexpr int GW = SK_NW * CW;                          // weight rows (columns) per group
+  static constexpr int BLK = SK_R * KK * 2;                      // one block of x rows
+  static constexpr int CH = KK * 2 / 16;                         // 16-byte chunks per row
+  static constexpr int DPW = SK_R * CH / (64 * SK_NW);           // x DMA instructions per wave per block
+  static constexpr int ST = (RES || KK > 320) ? 3 : 4;           // slots: ST - 1 blocks in flight
+  static constexpr int SLOT = (RES ? 2 : 1) * BLK;
   static constexpr int OB = RES ? 1 : 2;                         // output tiles
-  static constexpr int ON = EPI == 1 ? SK_N / 2 : SK_N;          // output columns per group
+  static constexpr int ON = EPI == 1 ? GW / 2 : GW;              // output columns per group
   static constexpr int OROW = ON + 8;                            // output tile row (elements)
   static constexpr int EPC = SK_R * (ON / 8) / SK_NT;            // output chunks per thread per block
   static constexpr int LDS = ST * SLOT + OB * SK_R * OROW * 2;
-  static constexpr int D = RES ? 4 : 2;                          // DMA instructions per wave per block
-  static_assert(SK_R * (ON / 8) == EPC * SK_NT, "whole chunks per thread");
+  static constexpr int D = (RES ? 2 : 1) * DPW;                  // DMA instructions per wave per block
+  // the in-order vmcnt that retires a wave's DMA of block li counts everything issued after it; in the
+  // steady state: for each of the next ST - 2 iterations its DMA and its EPC stores (and, with the
+  // residual's barrier before the stores, the stores of the iteration that issued it)
+  static constexpr int YOUNG = (RES ? EPC : 0) + (ST - 2) * (D + EPC);
+  static_assert(SK_R * CH == DPW * 64 * SK_NW && SK_R * (ON / 8) == EPC * SK_NT, "whole instructions / chunks");
+  static_assert(!RES || (KK == 320 && CW == 32 && EPI == 0), "a residual on the 320 x 320 stream only");
+  static_assert(EPI == 0 || (KK == 320 && CW == 32), "GEGLU: value and gate tiles in one wave");
+  static_assert(LDS <= 160 * 1024, "LDS");
+  // LDS slot of chunk c of row r: an XOR within aligned groups of 8 chunks (640-B rows: the 16 rows of
+  // a quarter-wave alternate two bank halves) or 16 (1280-B rows all start on bank 0)
+  __device__ static __forceinline__ int swz(int r, int c) {
+    if constexpr (KK == 320) return c ^ ((r >> 1) & 7);
+    else return c ^ (r & 15);
+  }
 };
 
-template <bool RES, int EPI>
+// one 1 KB lane-linear LDS-DMA (a non-template helper: see to_lds)
+__device__ __forceinline__ void sk_dma(__amdgpu_buffer_rsrc_t r, char* dst, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, to_lds(dst), 16, off, 0, 0, 0);
+}
+
+template <int KK, int CW, bool RES, int EPI>
 __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_args a) {
-  using S = SkCfg<RES, EPI>;
+  using S = SkCfg<KK, CW, RES, EPI>;
+  constexpr int CT = S::CT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = l & 15, fq = l >> 4;
   const int nblk = a.batch * a.out_h * a.out_w / SK_R;
-  const int NG = a.cout / SK_N;                                    // column groups
+  const int NG = a.cout / S::GW;                                   // column groups
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int cg = lid % NG, g = lid / NG, G = gridDim.x / NG;       // group, row-stream index, streams
   const int nmine = g < nblk ? (nblk - g + G - 1) / G : 0;
   bf16* Os = reinterpret_cast<bf16*>(smem + S::ST * S::SLOT);
-  const int ncol = cg * SK_N;                                      // this group's first weight row
+  const int ncol = cg * S::GW + CW * w;                            // this wave's first weight row
 
-  // this wave's 32 weight rows: all of K for them, as 16x16x32 B fragments (row ncol + 32 w + 16 t + fr,
+  // this wave's CW weight rows: all of K for them, as 16x16x32 B fragments (row ncol + 16 t + fr,
   // channels 32 s + 8 fq .. + 7)
   const bf16* wt = static_cast<const bf16*>(a.w);
-  bf16x8 wf[2][SK_K / 32];
+  bf16x8 wf[CT][KK / 32];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < CT; ++t)
 #pragma unroll
-    for (int s = 0; s < SK_K / 32; ++s)
-      wf[t][s] = *reinterpret_cast<const bf16x8*>(wt + (int64_t)(ncol + 32 * w + 16 * t + fr) * SK_K + 32 * s + 8 * fq);
+    for (int s = 0; s < KK / 32; ++s)
+      wf[t][s] = *reinterpret_cast<const bf16x8*>(wt + (int64_t)(ncol + 16 * t + fr) * KK + 32 * s + 8 * fq);
   const bf16* bias = static_cast<const bf16*>(a.bias);
-  float bv[2];
+  float bv[CT];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) bv[t] = bias ? (float)bias[ncol + 32 * w + 16 * t + fr] : 0.f;
+  for (int t = 0; t < CT; ++t) bv[t] = bias ? (float)bias[ncol + 16 * t + fr] : 0.f;
   const float al = a.alpha == 0.f ? 1.f : a.alpha;
 
-  // LDS-DMA: the block's 1280 16-byte slots, slot q = row * 40 + j holding chunk j ^ ((row >> 1) & 7)
-  // of the row (the XOR keeps the 16 rows of a ds_read_b128 quarter-wave on distinct bank groups);
-  // this wave fills slots [128 w, 128 w + 128), two lane-linear 1 KB instructions.  The residual's
-  // rows land unswizzled (the epilogue reads them as whole 16-byte chunks).
-  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (uint32_t)nblk * SK_BLK,
+  // LDS-DMA: the block's 16-byte slots q = row * CH + j, slot j of a row holding chunk swz(row, j);
+  // this wave fills DPW lane-linear 1 KB instructions.  The residual's rows land unswizzled (the
+  // epilogue reads them as whole 16-byte chunks).
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (uint32_t)nblk * S::BLK,
                                                                 0x00020000);
   __amdgpu_buffer_rsrc_t rr = xr;
   if constexpr (RES)
-    rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.residual), 0, (uint32_t)nblk * SK_BLK, 0x00020000);
-  uint32_t loff[2];
+    rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.residual), 0, (uint32_t)nblk * S::BLK, 0x00020000);
+  uint32_t loff[S::DPW];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int q = (2 * w + k) * 64 + l, row = q / SK_CH, j = q - row * SK_CH;
-    loff[k] = (uint32_t)(row * SK_K * 2 + (j ^ ((row >> 1) & 7)) * 16);
+  for (int k = 0; k < S::DPW; ++k) {
+    const int q = (S::DPW * w + k) * 64 + l, row = q / S::CH, j = q - row * S::CH;
+    loff[k] = (uint32_t)(row * KK * 2 + S::swz(row, j) * 16);
   }
   auto dma = [&](int li) {
-    const uint32_t base = (uint32_t)(g + li * G) * SK_BLK;
+    const uint32_t base = (uint32_t)(g + li * G) * S::BLK;
     char* st = smem + (li % S::ST) * S::SLOT;
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, to_lds(st + (2 * w + k) * 1024), 16, base + loff[k], 0, 0, 0);
+    for (int k = 0; k < S::DPW; ++k) sk_dma(xr, st + (S::DPW * w + k) * 1024, base + loff[k]);
     if constexpr (RES)
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, to_lds(st + SK_BLK + (2 * w + k) * 1024), 16,
-                                                 base + ((2 * w + k) * 64 + l) * 16, 0, 0, 0);
+      for (int k = 0; k < S::DPW; ++k)
+        sk_dma(rr, st + S::BLK + (S::DPW * w + k) * 1024, base + ((S::DPW * w + k) * 64 + l) * 16);
   };
-  // the in-order vmcnt that retires this wave's DMA of block li counts everything issued after it; in
-  // the steady state: for each of the next ST - 2 iterations its DMA and its EPC stores (and, with the
-  // residual's barrier before the stores, the stores of the iteration that issued it).  The first
-  // ST - 1 blocks and the tail wait for all.
-  constexpr int kYoung = (RES ? S::EPC : 0) + (S::ST - 2) * (S::D + S::EPC);
-  static_assert(kYoung == 8 || kYoung == 6, "the immediates below");
+  static_assert(S::YOUNG == 8 || S::YOUNG == 6 || S::YOUNG == 5, "the immediates below");
 #pragma unroll
   for (int p = 0; p < S::ST - 1; ++p)
     if (p < nmine) dma(p);
@@ -786,7 +803,7 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
       const int c = tid + k * SK_NT, row = c / (S::ON / 8), ch = c - row * (S::ON / 8);
       bf16x8 v = *reinterpret_cast<const bf16x8*>(O + row * S::OROW + ch * 8);
       if constexpr (RES) {
-        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(sl + SK_BLK + c * 16);
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(sl + S::BLK + c * 16);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)rv[j]);
       }
@@ -795,8 +812,9 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
   };
   for (int li = 0; li < nmine; ++li) {
     if (li >= S::ST - 1 && li + S::ST - 2 < nmine) {             // wave-uniform
-      if constexpr (kYoung == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if constexpr (S::YOUNG == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if constexpr (S::YOUNG == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -806,21 +824,21 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
       if (li > 0) store(li - 1, (li - 1) & 1, nullptr);
     if (li + S::ST - 1 < nmine) dma(li + S::ST - 1);               // into the slot block li - 1 used
     const char* st = smem + (li % S::ST) * S::SLOT;
-    f32x4v acc[2][2];
+    f32x4v acc[2][CT];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[i][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < CT; ++t) acc[i][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < SK_K / 32; ++s) {
+    for (int s = 0; s < KK / 32; ++s) {
       bf16x8 af[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = 16 * i + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(st + row * SK_K * 2 + ((4 * s + fq) ^ ((row >> 1) & 7)) * 16);
+        af[i] = *reinterpret_cast<const bf16x8*>(st + row * KK * 2 + S::swz(row, 4 * s + fq) * 16);
       }
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < CT; ++t) {
         acc[0][t] = mfma16(af[0], wf[t][s], acc[0][t]);
         acc[1][t] = mfma16(af[1], wf[t][s], acc[1][t]);
       }
@@ -834,7 +852,7 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const f32x4v val = round_bf16x4(acc[i][0] + bv[0]);
-        const f32x4v gt = round_bf16x4(acc[i][1] + bv[1]);
+        const f32x4v gt = round_bf16x4(acc[i][CT - 1] + bv[CT - 1]);
         const f32x4v ge = round_bf16x4(gt * 0.5f * (1.f + erf_fast4(gt * kAlpha)));
         const f32x4v o = val * ge;
 #pragma unroll
@@ -845,11 +863,11 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < CT; ++t) {
           const f32x4v v = (acc[i][t] + bv[t]) * al;
           const bf16x2v lo = __builtin_convertvector(f32x2v{v[0], v[1]}, bf16x2v);
           const bf16x2v hi = __builtin_convertvector(f32x2v{v[2], v[3]}, bf16x2v);
-          bf16* c = O + (16 * i + 4 * fq) * S::OROW + 32 * w + 16 * t + fr;
+          bf16* c = O + (16 * i + 4 * fq) * S::OROW + CW * w + 16 * t + fr;
           c[0] = lo.x;
           c[S::OROW] = lo.y;
           c[2 * S::OROW] = hi.x;
@@ -871,23 +889,34 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
   }
 }
 
-template <bool RES, int EPI>
-static int launch_k320(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
-  constexpr int lds = SkCfg<RES, EPI>::LDS;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_k320<RES, EPI>),
+template <int KK, int CW, bool RES, int EPI>
+static int launch_k320(const vp2p_conv_args& a, hipStream_t s, int n_cu) {
+  using S = SkCfg<KK, CW, RES, EPI>;
+  constexpr int lds = S::LDS;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_k320<KK, CW, RES, EPI>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
-  hipLaunchKernelGGL((conv_kernel_k320<RES, EPI>), grid, dim3(SK_NT), lds, s, a);
+  const int ng = a.cout / S::GW;
+  const int64_t nblk = (int64_t)a.batch * a.out_h * a.out_w / SK_R;
+  int64_t streams = n_cu / ng > 0 ? n_cu / ng : 1;                 // row streams per column group
+  if (streams > nblk) streams = nblk;
+  hipLaunchKernelGGL((conv_kernel_k320<KK, CW, RES, EPI>), dim3((unsigned)(streams * ng)), dim3(SK_NT), lds, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
-// the K10s shapes: a 1x1 GEMM with K = 320 and N = 320 NG (NG <= 8; a residual only at N = 320; the
-// plain or the GEGLU epilogue) on whole 32-row blocks, enough of them to give every CU a stream
-static bool skinny_ok(const vp2p_conv_args* a, int64_t M) {
-  return VP2P_K10_SKINNY && a->kernel == 1 && a->stride == 1 && a->cin == SK_K && a->cout % SK_N == 0 &&
-         a->cout <= 8 * SK_N && (!a->residual || a->cout == SK_N) && !a->x2 && !a->cin2 && !a->upsample &&
-         (a->epilogue == VP2P_CONV_EPI_NONE || a->epilogue == VP2P_CONV_EPI_GEGLU) && !a->gn_partials &&
-         !a->img_add && M % SK_R == 0 && M / SK_R >= 1024 && M * SK_K * 2 < ((int64_t)1 << 31);  // 32-bit offsets
+// the K10s shapes, on whole 32-row blocks, enough of them to give every CU a stream: 1x1, K = 320 and
+// N = 320 NG (NG <= 8; a residual only at N = 320; the plain or the GEGLU epilogue).  (The K = 640
+// form, SkCfg<640, 16, ...>, measured level with the tiled kernels on M 32768 K 640 N 640, 39.4 vs
+// 39.7 us, bit-equal, and is not dispatched: profiles/r05_k10s_k640_level.jsonl.)
+static int skinny_kind(const vp2p_conv_args* a, int64_t M) {
+  if (!VP2P_K10_SKINNY || a->kernel != 1 || a->stride != 1 || a->x2 || a->cin2 || a->upsample || a->gn_partials ||
+      a->img_add || M % SK_R || M / SK_R < 1024 || M * a->cin * 2 >= ((int64_t)1 << 31))   // 32-bit offsets
+    return 0;
+  const bool plain = a->epilogue == VP2P_CONV_EPI_NONE;
+  if (a->cin == 320 && a->cout % 320 == 0 && a->cout <= 2560 && (plain || a->epilogue == VP2P_CONV_EPI_GEGLU) &&
+      (!a->residual || (a->cout == 320 && plain)))
+    return 320;
+  return 0;
 }
 
 template <int KS, int EPI, int AM, int CF> struct ConvKernel;
@@ -1112,8 +1141,7 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   if (tiles * k > 0x7fffffff) return VP2P_E_SHAPE;
   const dim3 grid((unsigned)(tiles * k));
   int rc;
-  if (conv::skinny_ok(a, M)) {
-    const int ng = a->cout / conv::SK_N;
+  if (const int sk = conv::skinny_kind(a, M); sk) {
     static int n_cu = 0;
     if (!n_cu) {
       int dev = 0;
@@ -1121,13 +1149,9 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
           hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
         n_cu = 256;
     }
-    const int64_t nblk = M / conv::SK_R;
-    int64_t streams = n_cu / ng > 0 ? n_cu / ng : 1;               // row streams per column group
-    if (streams > nblk) streams = nblk;
-    const dim3 gk((unsigned)(streams * ng));
-    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_k320<false, 1>(*a, gk, s);
-    else if (a->residual) rc = conv::launch_k320<true, 0>(*a, gk, s);
-    else rc = conv::launch_k320<false, 0>(*a, gk, s);
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_k320<320, 32, false, 1>(*a, s, n_cu);
+    else if (a->residual) rc = conv::launch_k320<320, 32, true, 0>(*a, s, n_cu);
+    else rc = conv::launch_k320<320, 32, false, 0>(*a, s, n_cu);
   } else if (k > 1) {
     vp2p_conv_args b = *a;
     b.ksplit = k;
