@@ -685,6 +685,9 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_s(const vp2p_conv_args a) 
 #ifndef VP2P_K10_SKINNY
 #define VP2P_K10_SKINNY 1
 #endif
+#ifndef VP2P_K10S_MINBLK      // the fewest 32-row blocks the stream takes (fewer: the tiled kernels)
+#define VP2P_K10S_MINBLK 1024
+#endif
 constexpr int SK_R = 32, SK_NW = 10, SK_NT = 64 * SK_NW;
 // ring slots: x (and, with a residual, the residual's rows too, also by LDS-DMA: a register load of
 // it would be the youngest vector-memory operation, and waiting for it drains the x prefetch).
@@ -910,7 +913,7 @@ static int launch_k320(const vp2p_conv_args& a, hipStream_t s, int n_cu) {
 // 39.7 us, bit-equal, and is not dispatched: profiles/r05_k10s_k640_level.jsonl.)
 static int skinny_kind(const vp2p_conv_args* a, int64_t M) {
   if (!VP2P_K10_SKINNY || a->kernel != 1 || a->stride != 1 || a->x2 || a->cin2 || a->upsample || a->gn_partials ||
-      a->img_add || M % SK_R || M / SK_R < 1024 || M * a->cin * 2 >= ((int64_t)1 << 31))   // 32-bit offsets
+      a->img_add || M % SK_R || M / SK_R < VP2P_K10S_MINBLK || M * a->cin * 2 >= ((int64_t)1 << 31))   // 32-bit offsets
     return 0;
   const bool plain = a->epilogue == VP2P_CONV_EPI_NONE;
   if (a->cin == 320 && a->cout % 320 == 0 && a->cout <= 2560 && (plain || a->epilogue == VP2P_CONV_EPI_GEGLU) &&
