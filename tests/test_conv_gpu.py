@@ -353,3 +353,4 @@ def test_k10_stream_k320_groups(M, N, geglu):
     err = (full[:4096].float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-2, err
 
+

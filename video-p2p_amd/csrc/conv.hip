@@ -688,7 +688,7 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_s(const vp2p_conv_args a) 
 #ifndef VP2P_K10S_MINBLK      // the fewest 32-row blocks the stream takes (fewer: the tiled kernels)
 #define VP2P_K10S_MINBLK 1024
 #endif
-constexpr int SK_R = 32, SK_NW = 10, SK_NT = 64 * SK_NW;
+constexpr int SK_R = 32;
 // ring slots: x (and, with a residual, the residual's rows too, also by LDS-DMA: a register load of
 // it would be the youngest vector-memory operation, and waiting for it drains the x prefetch).
 // Without a residual the output tile is double-buffered and block li's rows are stored after the
@@ -700,25 +700,26 @@ constexpr int SK_R = 32, SK_NW = 10, SK_NT = 64 * SK_NW;
 // 160-column groups, 40 KB blocks in a 3-slot ring; a wave's A fragments then feed one 16-column
 // tile each, so that stream is bound by LDS reads at half the MFMA rate (measured level with the
 // tiled kernels; not dispatched, see skinny_kind).
-template <int KK, int CW, bool RES, int EPI> struct SkCfg {
+template <int KK, int CW, bool RES, int EPI, int NW_ = 10> struct SkCfg {
+  static constexpr int NW = NW_, NT = 64 * NW;                   // waves, threads
   static constexpr int CT = CW / 16;                             // 16-column MFMA tiles per wave
-  static constexpr int GW = SK_NW * CW;                          // weight rows (columns) per group
+  static constexpr int GW = NW * CW;                             // weight rows (columns) per group
   static constexpr int BLK = SK_R * KK * 2;                      // one block of x rows
   static constexpr int CH = KK * 2 / 16;                         // 16-byte chunks per row
-  static constexpr int DPW = SK_R * CH / (64 * SK_NW);           // x DMA instructions per wave per block
+  static constexpr int DPW = SK_R * CH / (64 * NW);              // x DMA instructions per wave per block
   static constexpr int ST = (RES || KK > 320) ? 3 : 4;           // slots: ST - 1 blocks in flight
   static constexpr int SLOT = (RES ? 2 : 1) * BLK;
   static constexpr int OB = RES ? 1 : 2;                         // output tiles
   static constexpr int ON = EPI == 1 ? GW / 2 : GW;              // output columns per group
   static constexpr int OROW = ON + 8;                            // output tile row (elements)
-  static constexpr int EPC = SK_R * (ON / 8) / SK_NT;            // output chunks per thread per block
+  static constexpr int EPC = SK_R * (ON / 8) / NT;               // output chunks per thread per block
   static constexpr int LDS = ST * SLOT + OB * SK_R * OROW * 2;
   static constexpr int D = (RES ? 2 : 1) * DPW;                  // DMA instructions per wave per block
   // the in-order vmcnt that retires a wave's DMA of block li counts everything issued after it; in the
   // steady state: for each of the next ST - 2 iterations its DMA and its EPC stores (and, with the
   // residual's barrier before the stores, the stores of the iteration that issued it)
   static constexpr int YOUNG = (RES ? EPC : 0) + (ST - 2) * (D + EPC);
-  static_assert(SK_R * CH == DPW * 64 * SK_NW && SK_R * (ON / 8) == EPC * SK_NT, "whole instructions / chunks");
+  static_assert(SK_R * CH == DPW * 64 * NW && SK_R * (ON / 8) == EPC * NT, "whole instructions / chunks");
   static_assert(!RES || (KK == 320 && CW == 32 && EPI == 0), "a residual on the 320 x 320 stream only");
   static_assert(EPI == 0 || (KK == 320 && CW == 32), "GEGLU: value and gate tiles in one wave");
   static_assert(LDS <= 160 * 1024, "LDS");
@@ -735,9 +736,9 @@ __device__ __forceinline__ void sk_dma(__amdgpu_buffer_rsrc_t r, char* dst, uint
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, to_lds(dst), 16, off, 0, 0, 0);
 }
 
-template <int KK, int CW, bool RES, int EPI>
-__global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_args a) {
-  using S = SkCfg<KK, CW, RES, EPI>;
+template <int KK, int CW, bool RES, int EPI, int NW = 10>
+__global__ __launch_bounds__(64 * NW, 1) void conv_kernel_k320(const vp2p_conv_args a) {
+  using S = SkCfg<KK, CW, RES, EPI, NW>;
   constexpr int CT = S::CT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, l = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -789,7 +790,7 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
       for (int k = 0; k < S::DPW; ++k)
         sk_dma(rr, st + S::BLK + (S::DPW * w + k) * 1024, base + ((S::DPW * w + k) * 64 + l) * 16);
   };
-  static_assert(S::YOUNG == 8 || S::YOUNG == 6 || S::YOUNG == 5, "the immediates below");
+  static_assert(S::YOUNG == 10 || S::YOUNG == 8 || S::YOUNG == 6, "the immediates below");
 #pragma unroll
   for (int p = 0; p < S::ST - 1; ++p)
     if (p < nmine) dma(p);
@@ -803,7 +804,7 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
     const int64_t r0 = (int64_t)(g + lj * G) * SK_R;
 #pragma unroll
     for (int k = 0; k < S::EPC; ++k) {
-      const int c = tid + k * SK_NT, row = c / (S::ON / 8), ch = c - row * (S::ON / 8);
+      const int c = tid + k * S::NT, row = c / (S::ON / 8), ch = c - row * (S::ON / 8);
       bf16x8 v = *reinterpret_cast<const bf16x8*>(O + row * S::OROW + ch * 8);
       if constexpr (RES) {
         const bf16x8 rv = *reinterpret_cast<const bf16x8*>(sl + S::BLK + c * 16);
@@ -815,9 +816,9 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
   };
   for (int li = 0; li < nmine; ++li) {
     if (li >= S::ST - 1 && li + S::ST - 2 < nmine) {             // wave-uniform
-      if constexpr (S::YOUNG == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if constexpr (S::YOUNG == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      if constexpr (S::YOUNG == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if constexpr (S::YOUNG == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -892,25 +893,28 @@ __global__ __launch_bounds__(SK_NT, 1) void conv_kernel_k320(const vp2p_conv_arg
   }
 }
 
-template <int KK, int CW, bool RES, int EPI>
+template <int KK, int CW, bool RES, int EPI, int NW = 10>
 static int launch_k320(const vp2p_conv_args& a, hipStream_t s, int n_cu) {
-  using S = SkCfg<KK, CW, RES, EPI>;
+  using S = SkCfg<KK, CW, RES, EPI, NW>;
   constexpr int lds = S::LDS;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_k320<KK, CW, RES, EPI>),
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel_k320<KK, CW, RES, EPI, NW>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   if (!attr) return VP2P_E_LAUNCH;
   const int ng = a.cout / S::GW;
   const int64_t nblk = (int64_t)a.batch * a.out_h * a.out_w / SK_R;
   int64_t streams = n_cu / ng > 0 ? n_cu / ng : 1;                 // row streams per column group
   if (streams > nblk) streams = nblk;
-  hipLaunchKernelGGL((conv_kernel_k320<KK, CW, RES, EPI>), dim3((unsigned)(streams * ng)), dim3(SK_NT), lds, s, a);
+  hipLaunchKernelGGL((conv_kernel_k320<KK, CW, RES, EPI, NW>), dim3((unsigned)(streams * ng)), dim3(S::NT), lds, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
 // the K10s shapes, on whole 32-row blocks, enough of them to give every CU a stream: 1x1, K = 320 and
-// N = 320 NG (NG <= 8; a residual only at N = 320; the plain or the GEGLU epilogue).  (The K = 640
-// form, SkCfg<640, 16, ...>, measured level with the tiled kernels on M 32768 K 640 N 640, 39.4 vs
-// 39.7 us, bit-equal, and is not dispatched: profiles/r05_k10s_k640_level.jsonl.)
+// N = 320 NG (NG <= 8; a residual only at N = 320; the plain or the GEGLU epilogue).  (K = 640 forms,
+// bit-equal, measured level with the tiled kernels on M 32768 K 640 N 640 and are not dispatched:
+// 10 waves x 16 rows (SkCfg<640, 16, ...>, LDS-read bound) 39.4 vs 39.7 us,
+// profiles/r05_k10s_k640_level.jsonl; 5 waves x 32 rows (SkCfg<640, 32, false, 0, 5>, W in 160 VGPRs,
+// one SIMD with two waves against three with one) 39.0 vs 39.2 us and the edit 0.5 % slower,
+// profiles/r05_k10s_k640_5w_rejected.jsonl.)
 static int skinny_kind(const vp2p_conv_args* a, int64_t M) {
   if (!VP2P_K10_SKINNY || a->kernel != 1 || a->stride != 1 || a->x2 || a->cin2 || a->upsample || a->gn_partials ||
       a->img_add || M % SK_R || M / SK_R < VP2P_K10S_MINBLK || M * a->cin * 2 >= ((int64_t)1 << 31))   // 32-bit offsets
