@@ -17,6 +17,11 @@
 //    16-byte zero vector for padding taps), B rows 128 bytes of weight rows, moved by LDS-DMA
 //    (global_load_lds_dwordx4) into two LDS stages; one barrier per step, the DMA of step s+1 runs
 //    under the MFMAs of step s and no VGPR holds the tile in flight;
+//  * K order channel-major (round 5): the nine taps of one 64-channel chunk in consecutive steps,
+//    so a chunk's shifted re-reads (one 128-B line per pixel) hit L2.  Tap-major (all channels of
+//    a tap, then the next) spans 640-2560 B per pixel between re-reads, over the 4 MB L2 of an XCD
+//    at 32 concurrent tiles: FETCH + WRITE 934 -> 281 MB per 64^2 320 -> 320 launch (3.7x -> 1.1x the
+//    algorithmic bytes), 0.238 -> 0.222 ms, whole edit +1.4 % (profiles/r05_k10_cmajor_*);
 //  * LDS rows are unpadded 128 B; the XOR swizzle (slot j of row r holds chunk j ^ ((r >> 1) & 7))
 //    is applied on the per-lane DMA source address, so the 16 rows a 16-lane ds_read_b128 touches
 //    fall in 16 distinct 4-bank groups;
@@ -51,6 +56,11 @@ namespace conv {
 #define VP2P_K10_PIPE 1
 #endif
 constexpr bool kPipe = VP2P_K10_PIPE;
+// K order of the KS x KS convs: 0 tap-major (all channels of one tap, then the next tap), 1
+// channel-major (the taps of one 64-channel chunk in consecutive steps)
+#ifndef VP2P_K10_CMAJOR
+#define VP2P_K10_CMAJOR 1
+#endif
 
 constexpr int BN = 160, BK = 64;
 constexpr int CROW = BN + 8;                    // epilogue tile row (elements)
@@ -320,7 +330,13 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   const int nall = KS * KS * csteps;
   const int s_begin = (int)((int64_t)nall * split / ks_n), s_end = (int)((int64_t)nall * (split + 1) / ks_n);
   auto dma = [&](int step, int stage) {
+#if VP2P_K10_CMAJOR
+    // channel-major K order: the KS x KS taps of one 64-channel chunk in consecutive steps, so the
+    // shifted re-reads of a chunk's rows (128 B, one L2 line) hit L2
+    const int cs = KS == 1 ? step : step / (KS * KS), tap = step - cs * (KS * KS), c0 = cs * Cfg::KB;
+#else
     const int tap = step / csteps, c0 = (step - tap * csteps) * Cfg::KB;
+#endif
     const int kh = tap / KS, kw = tap - kh * KS;
     char* As = smem + stage * Cfg::STAGE;
     char* Bs = As + Cfg::TBM * Cfg::RB;
