@@ -61,6 +61,14 @@ constexpr bool kPipe = VP2P_K10_PIPE;
 #ifndef VP2P_K10_CMAJOR
 #define VP2P_K10_CMAJOR 1
 #endif
+// tile raster of the one-pass grids (split-K keeps row-major): 0 row tile major (all column tiles
+// of a row tile in consecutive workgroups), G > 0 grouped (G row tiles per group, row tile
+// fastest), so an XCD's contiguous share of the grid reads fewer weight columns.  Same tiles, so
+// bit-equal; 8 measured 0-5 % faster per launch (res-32 GEGLU 0.242 -> 0.231 ms, 64^2 640 -> 320
+// 3x3 0.401 -> 0.391 ms; profiles/r05_k10_groupm_ab.jsonl), the whole edit +0.3 %
+#ifndef VP2P_K10_GROUPM
+#define VP2P_K10_GROUPM 8
+#endif
 
 constexpr int BN = 160, BK = 64;
 constexpr int CROW = BN + 8;                    // epilogue tile row (elements)
@@ -251,7 +259,23 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
   const int ks_n = EPI == 2 ? a.ksplit : 1;
   const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid0 % ks_n, bid = bid0 / ks_n;
+#if VP2P_K10_GROUPM > 0
+  // grouped raster: GROUPM row tiles x all column tiles per group, row tile fastest, so an XCD's
+  // contiguous share of the grid covers GROUPM rows x a few columns (fewer weight bytes per XCD)
+  int mt, nt;
+  if (ks_n == 1) {
+    const int mtn = (M + Cfg::TBM - 1) / Cfg::TBM;
+    const int per = VP2P_K10_GROUPM * ntn, g = bid / per, first = g * VP2P_K10_GROUPM;
+    const int gs = min(mtn - first, VP2P_K10_GROUPM), in = bid - g * per;
+    mt = first + in % gs;
+    nt = in / gs;
+  } else {
+    mt = bid / ntn;
+    nt = bid - mt * ntn;
+  }
+#else
   const int mt = bid / ntn, nt = bid - mt * ntn;
+#endif
   const int m0 = mt * Cfg::TBM, n0 = nt * Cfg::TBN;
   const bf16* x = static_cast<const bf16*>(a.x);
   const bf16* wt = static_cast<const bf16*>(a.w);
