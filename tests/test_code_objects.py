@@ -10,7 +10,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "video-p2p_amd", "lib", "libvp2p_hip.so")
+LIB = os.environ.get("VP2P_LIB") or os.path.join(ROOT, "video-p2p_amd", "lib", "libvp2p_hip.so")
 READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
