@@ -323,7 +323,7 @@ def test_k10_stream_k320(M, epi):
 
 
 @pytest.mark.parametrize("M,N,geglu", [(131072, 960, False), (131072, 2560, True), (393216, 2560, True),
-                                       (98336, 960, False)])
+                                       (98336, 960, False), (98336, 2560, True)])
 def test_k10_stream_k320_groups(M, N, geglu):
     """K10s over N = 320 NG column groups: attn_temp's q|k|v (N 960) and the GEGLU projection (N 2560,
     interleaved weights, the GEGLU epilogue; 8 and 24 frames) -- bit-equal to the tiled kernels on

@@ -509,6 +509,8 @@ __device__ __forceinline__ void conv_tile(const vp2p_conv_args& a) {
       };
       auto ldH = [&](int ks, int k) { return HB ? ldB(ks, k) : ldA(ks, k); };
       auto ldR = [&](int ks, int k) { return HB ? ldA(ks, k) : ldB(ks, k); };
+      // R[1] below is fragment (ks 0, idx 1): the rotation assumes two fragments per k-step
+      static_assert(NR >= 2, "pipelined fragment reads need NR = max(WTM, WTN) >= 2");
       bf16x8 H[2][NH], R[3];
 #pragma unroll
       for (int k = 0; k < NH; ++k) H[0][k] = ldH(0, k);
@@ -1202,12 +1204,16 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   const dim3 grid((unsigned)(tiles * k));
   int rc;
   if (const int sk = conv::skinny_kind(a, M); sk) {
-    static int n_cu = 0;
+    // the persistent grid is sized by the CU count of the device this launch runs on (cached per
+    // device id: a process may drive several devices)
+    static int n_cu_of[64] = {};
+    int dev = 0, n_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    if (dev < 64) n_cu = n_cu_of[dev];
     if (!n_cu) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
         n_cu = 256;
+      if (dev < 64) n_cu_of[dev] = n_cu;
     }
     if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_k320<320, 32, false, 1>(*a, s, n_cu);
     else if (a->residual) rc = conv::launch_k320<320, 32, true, 0>(*a, s, n_cu);

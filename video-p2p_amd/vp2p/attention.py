@@ -413,6 +413,11 @@ def _frame_forward(net):
             raise NotImplementedError("FrameAttention: group_norm / added_kv_proj_dim")
         if video_length is None:
             raise ValueError("FrameAttention needs video_length (attention.py:293)")
+        if hidden_states.dtype not in (torch.float32, torch.bfloat16):
+            # K1 computes in fp32 or bf16; an fp16 reference UNet (run_videop2p.py:93 mixed
+            # precision) is not supported
+            raise NotImplementedError(f"FrameAttention on the HIP kernels: dtype {hidden_states.dtype} "
+                                      "(supported: torch.float32, torch.bfloat16)")
         return FrameAttention.forward(net, hidden_states, encoder_hidden_states, attention_mask,
                                       video_length, residual)
     return forward

@@ -20,6 +20,7 @@ import hashlib
 import os
 import shutil
 import tempfile
+import warnings
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 MIOPEN_DB = os.path.join(ROOT, "miopen_db")
@@ -41,11 +42,12 @@ def seeded_cache_dir() -> str:
     files would modify the checkout and fail on a read-only one.  The copy is keyed by the in-tree
     files' content: a changed database gets a fresh copy, the committed files are never written."""
     files = _seed_files()
+    # keyed by name, size and mtime (not a hash of every byte: the kernel cache is tens of MB and
+    # every rank of every process start would read it)
     h = hashlib.sha1()
     for src, rel in files:
-        h.update(rel.encode())
-        with open(src, "rb") as fh:
-            h.update(fh.read())
+        st = os.stat(src)
+        h.update(f"{rel}:{st.st_size}:{st.st_mtime_ns}".encode())
     base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
     try:
         os.makedirs(base, exist_ok=True)
@@ -62,8 +64,15 @@ def seeded_cache_dir() -> str:
             shutil.copy2(src, os.path.join(tmp, rel))
         try:
             os.rename(tmp, dst)          # atomic; a concurrent process may have won the race
-        except OSError:
-            shutil.rmtree(tmp, ignore_errors=True)
+        except OSError as e:
+            if os.path.isdir(dst):       # lost the race: the winner's copy is the same content
+                shutil.rmtree(tmp, ignore_errors=True)
+            else:                        # EXDEV, permissions, ...: keep using the private copy
+                warnings.warn(f"vp2p.tuning: could not publish the MIOpen seed copy at {dst} ({e}); "
+                              f"using {tmp}")
+                return tmp
+    if not os.path.isdir(dst):
+        raise RuntimeError(f"vp2p.tuning: MIOpen seed directory {dst} is missing")
     return dst
 
 
