@@ -37,9 +37,10 @@ UNET_EDIT_STEPS = (0, 45)          # controller cur_step of the two controlled f
 EDITS = {
     "car2": ("car", 2, 12, (0, 9, 10, 11)),
     "rabbit8": ("rabbit", 8, 50, (0, 10, 11, 24, 25, 49)),
-    # configs[2] past the self-replace boundary (self_replace_steps 0.5 of 50: steps 24 / 25) to step 26
-    # (round 5; replaces round 3's 12-step "penguin24", whose fixture saved steps 10 / 11 only)
-    "penguin24l": ("penguin", 24, 27, (10, 11, 24, 25, 26)),
+    # configs[2], all 50 steps: across the self-replace boundary (self_replace_steps 0.5 of 50: steps
+    # 24 / 25) and through the last LocalBlend-driven step 49 (round 6; round 5's fixture stopped at
+    # step 26, round 3's "penguin24" at step 11)
+    "penguin24l": ("penguin", 24, 50, (10, 11, 24, 25, 26, 49)),
 }
 
 

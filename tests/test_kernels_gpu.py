@@ -283,6 +283,58 @@ def test_temporal_attention_p2p(tokenizer, dtype, frames, d, step):
     assert torch.equal(out_bd.cpu().float(), torch.from_numpy(got))
 
 
+@pytest.mark.parametrize("mode,n", [("edit", 4096), ("replace", 4096), ("cond_only", 4096), ("plain2", 4096),
+                                    ("replace", 4100), ("plain4", 2050)])
+def test_temporal_stream(tokenizer, mode, n):
+    """K3s, the persistent res-64 stream (bf16, d 40, 8 frames, q|k|v slices of one projection as the
+    UNet calls it): the same numbers as the short kernel (VP2P_K3_STREAM=0), and the oracle on the
+    P2P cases -- edit / self-replace / the CFG-split conditional half / plain row pairs, and ragged
+    item counts (tokens 4100, 2050) that leave the persistent grid's last round partial."""
+    import os
+    from vp2p import ops
+    heads, d, frames = 8, 40, 8
+    C = heads * d
+    P = 2
+    B = {"edit": 4, "replace": 4, "cond_only": 2, "plain2": 2, "plain4": 4}[mode]
+    g = torch.Generator().manual_seed(77)
+    qkv = (torch.randn(B * frames, n, 3 * C, generator=g) * 2.0).to(torch.bfloat16).to(DEV)
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    kw = {}
+    if mode in ("edit", "replace", "cond_only"):
+        kw = dict(prompts=P, self_replace=mode != "edit", cond_only=mode == "cond_only")
+
+    def run(stream):
+        old = os.environ.get("VP2P_K3_STREAM")
+        os.environ["VP2P_K3_STREAM"] = "1" if stream else "0"
+        try:
+            out = ops.temporal_attention_p2p(q, k, v, frames, heads, **kw)
+            torch.cuda.synchronize()
+        finally:
+            if old is None:
+                del os.environ["VP2P_K3_STREAM"]
+            else:
+                os.environ["VP2P_K3_STREAM"] = old
+        return out.float().cpu()
+    got, short = run(True), run(False)
+    # same MFMAs / softmax roundings; only the zero-padded key positions inside a 16-key MFMA step
+    # differ between the two packings, so allow the last bit
+    diff = (got - short).abs().max().item()
+    assert diff <= 2 ** -7 * short.abs().max().item(), diff
+    if mode in ("edit", "replace", "cond_only"):
+        ctrl = _controller(tokenizer, "rabbit", 30 if mode == "edit" else 0)
+        nt = 64                                   # the oracle on the first 64 tokens
+        sub = lambda t: t[:, :nt].float().cpu().numpy().reshape(B, frames, nt, C).transpose(0, 2, 1, 3).reshape(B * nt, frames, C)  # noqa
+        if mode == "cond_only":
+            # the conditional half alone: the oracle runs the whole [uncond, cond] batch
+            full = lambda t: np.concatenate([sub(t), sub(t)])                                             # noqa
+            ref, _ = O.controlled_core(full(q), full(k), full(v), heads, False, ctrl, "down")
+            ref = ref[B * nt:]
+        else:
+            ref, _ = O.controlled_core(sub(q), sub(k), sub(v), heads, False, ctrl, "down")
+        g2 = got[:, :nt].numpy().reshape(B, frames, nt, C).transpose(0, 2, 1, 3).reshape(B * nt, frames, C)
+        assert _rel(g2, ref) < TOL[torch.bfloat16], _rel(g2, ref)
+
+
 # ------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("t,fast,blend", [(981, True, True), (501, False, True), (21, True, False),
                                           (501, True, "substruct")])
