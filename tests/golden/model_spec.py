@@ -44,6 +44,17 @@ EDITS = {
 }
 
 
+def edit_schedule(name: str, gold=None):
+    """(steps to run, steps whose latents are compared) for an end-to-end edit: from the fixture when
+    one is given (its ``steps_run`` and saved ``latents/<i>``), so a fixture generated for an older
+    EDITS entry still checks what it holds; else EDITS[name]."""
+    _, _, steps, save = EDITS[name]
+    if gold is not None:
+        steps = int(gold["steps_run"])
+        save = tuple(sorted(int(k.split("/")[1]) for k in gold.files if k.startswith("latents/")))
+    return steps, save
+
+
 # Null-text optimisation fixtures (run_videop2p.py:557-612): name -> (UNet3DConditionModel kwargs,
 # init_random_ std, x_0 shape (1, 4, f, h, w), DDIM steps, max inner Adam iterations)
 NULLTEXT = {

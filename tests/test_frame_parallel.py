@@ -287,11 +287,11 @@ def test_frame_sharded_nulltext_matches_single(tmp_path):
 
 
 # ------------------------------------------------------------------------------------------------
-def _penguin_worker(rank, world, port, out_path):
+def _penguin_worker(rank, world, port, out_path, steps, save):
     """configs[2] (penguin-run refine edit, 24 frames, SD-1.5 geometry, bf16) under the bench's
     4-rank EditLayout: CFG split x 2 frame shards of 12 frames each (all ranks on the one GPU, gloo
-    with host staging).  Run to step 26 of 50, past the self-replace boundary (steps 24 / 25), the
-    steps the reference fixture saved (golden_edit_penguin24l.npz)."""
+    with host staging).  Run for the steps the reference fixture ran (golden_edit_penguin24l.npz: all 50,
+    past the self-replace boundary at 24 / 25), comparing the latents it saved."""
     dist = _init(rank, world, port)
     import model_spec as MS
     import spec
@@ -300,7 +300,7 @@ def _penguin_worker(rank, world, port, out_path):
     from vp2p.pipeline import VideoP2PPipeline
     from vp2p.tokenizer import SyntheticCLIPTokenizer
     from vp2p.unet3d import UNet3DConditionModel, init_random_
-    edit, f, steps, save = MS.EDITS["penguin24l"]
+    edit, f, _, _ = MS.EDITS["penguin24l"]
     prompts, swap, blend, eq, cross, self_ = spec.CONFIGS[edit]
     tok = SyntheticCLIPTokenizer()
     state = init_random_(UNet3DConditionModel(), seed=0).state_dict()
@@ -346,7 +346,7 @@ def _penguin_worker(rank, world, port, out_path):
 def test_sharded_penguin24_vs_reference(tmp_path):
     """SURVEY §8(e) at a real configuration: the 4-rank layout (CFG split x 2 frame shards) of the
     24-frame penguin refine edit against the reference pipeline's fixture (golden_edit_penguin24l.npz,
-    27 of 50 steps: latents at 10, 11 and across the self-replace boundary 24 / 25 / 26).  Bar: the
+    all 50 steps: latents at 10, 11, across the self-replace boundary 24 / 25 / 26, and the final 49).  Bar: the
     bf16 end-to-end bar, final-latent PSNR >= 45 dB, and at most 2 % of the LocalBlend mask pixels
     flipped against the reference (as for the single-rank case)."""
     import numpy as np
@@ -358,8 +358,8 @@ def test_sharded_penguin24_vs_reference(tmp_path):
         pytest.skip("golden_edit_penguin24l.npz not generated")
     gold = np.load(path)
     out = str(tmp_path / "penguin")
-    mp.spawn(_penguin_worker, args=(4, _port(), out), nprocs=4, join=True)
-    _, f, steps, save = MS.EDITS["penguin24l"]
+    steps, save = MS.edit_schedule("penguin24l", gold)
+    mp.spawn(_penguin_worker, args=(4, _port(), out, steps, save), nprocs=4, join=True)
     for r in range(4):
         got = torch.load(out + f".{r}")
         assert got["cur_step"] == int(gold["cur_step"]) and got["lb_counter"] == int(gold["lb_counter"]), r
