@@ -103,7 +103,7 @@ class FrameAttention(CrossAttention):
                   else torch.empty(B, *x.shape[1:], device=x.device, dtype=x.dtype))
             pending = (x0, shard.broadcast_async(x0))
         if differentiated:
-            q = F.linear(x, self.to_q.weight, self.to_q.bias)
+            q = ops.linear(x, self.to_q.weight, self.to_q.bias)
             prescaled = False
         else:
             # the softmax scale (times log2 e) rides in the projection GEMM's alpha: one rounding of
@@ -118,10 +118,10 @@ class FrameAttention(CrossAttention):
                 # frames sharded under autograd (null-text): rank 0's frame-0 hidden state, with the
                 # adjoint (its gradient summed over the ranks that projected K|V from it)
                 x0 = frame_parallel.frame0_hidden(shard, x0)
-            kv = F.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
-                          None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
+            kv = ops.linear(x0, _cat_weight(self, ("to_k", "to_v"), "_wkv"),
+                            None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias]))
             out = autograd.SharedKVAttention.apply(q, kv, f, self.heads, self.scale)
-            y = self.to_out[1](self.to_out[0](out))
+            y = self.to_out[1](_linear_out(self.to_out[0], out))
             return y if residual is None else y + residual
         wkv = _cat_weight(self, ("to_k", "to_v"), "_wkv")
         bkv = None if self.to_k.bias is None else torch.cat([self.to_k.bias, self.to_v.bias])
@@ -214,10 +214,10 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
             # differentiated (null-text optimisation): only the uncontrolled hook is ever traced there
             if not plain:
                 raise NotImplementedError("backward through a P2P-controlled attention layer")
-            q = F.linear(x, module.to_q.weight, module.to_q.bias)
-            kv = F.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
-                          None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))
-            y = to_out(autograd.SharedKVAttention.apply(q, kv, f, h, module.scale))
+            q = ops.linear(x, module.to_q.weight, module.to_q.bias)
+            kv = ops.linear(ctx, _cat_weight(module, ("to_k", "to_v"), "_wkv"),
+                            None if module.to_k.bias is None else torch.cat([module.to_k.bias, module.to_v.bias]))
+            y = _linear_out(to_out, autograd.SharedKVAttention.apply(q, kv, f, h, module.scale))
             return y if residual is None else y + residual
         q = ops.linear(x, module.to_q.weight, module.to_q.bias)
         k, v, kv_ws = _context_kv(module, ctx, h)
@@ -260,8 +260,8 @@ def hooked_attention(module, controller, place, x, context=None, attention_mask=
             Bq = x.shape[0] // video_length
             qkv = ops.linear(frame_parallel.to_tokens(sh, x, Bq), w, bias)
             out = autograd.TemporalAttention.apply(qkv, video_length * sh.world, h, module.scale)
-            return to_out(frame_parallel.to_frames(sh, out, Bq))
-        return to_out(autograd.TemporalAttention.apply(ops.linear(x, w, bias), video_length, h, module.scale))
+            return _linear_out(to_out, frame_parallel.to_frames(sh, out, Bq))
+        return _linear_out(to_out, autograd.TemporalAttention.apply(ops.linear(x, w, bias), video_length, h, module.scale))
     shard = frame_parallel.active() if temporal_layout == "bf" else None
     if shard is not None and shard.world <= 1:
         shard = None
@@ -322,9 +322,10 @@ def _plain_linear(m) -> bool:
 
 
 def _linear_out(to_out, out):
-    """``to_out(out)`` at inference through ``ops.linear`` (K10's GEMM core for the K = 320 projections
-    of the 64x64 latents, hipBLASLt elsewhere); any other module, or autograd, calls it as is."""
-    if _plain_linear(to_out) and not torch.is_grad_enabled():
+    """``to_out(out)`` through ``ops.linear`` (K10's GEMM core for the K = 320 projections of the 64x64
+    latents, hipBLASLt elsewhere; under autograd with frozen weights the same dispatch forward and
+    backward); any other module is called as is."""
+    if _plain_linear(to_out):
         return ops.linear(out, to_out.weight, to_out.bias)
     return to_out(out)
 

@@ -9,11 +9,19 @@ gets its backward as a HIP kernel too:
   and the plain hooked cross-attention (ptp_utils.py:206-220 under the DummyController)
 * ``TemporalAttention``  K3 forward / K3b backward -- plain hooked attn_temp (attention.py:262-268)
 * ``GroupNormFn``        K7 / K7b,  ``LayerNormFn`` K8 / K8b,  ``GEGLUFn`` K9 / K9b
+* ``FrozenLinear``       a projection with frozen weights: forward through ``ops.linear`` (K10's GEMM
+  core or hipBLASLt, per the in-tree table, as at inference), backward dx = dy @ W the same way
+* ``FrozenConv``         an InflatedConv3d with frozen weights: forward through the inference dispatch
+  (K10 per the in-tree table / MIOpen), backward dx on K10 as a forward convolution (3x3 stride 1:
+  dy * the flipped, transposed kernel; 1x1: dy @ W), MIOpen's backward-data elsewhere
 
 Frame-sharded (``frame_parallel``): every cross-frame coupling has a differentiable exchange --
 ``GroupNormFn`` gathers forward and backward statistics partials, FrameAttention's frame-0 hidden
 state and attn_temp's all-to-alls carry their adjoints (``frame_parallel.frame0_hidden`` /
 ``to_tokens`` / ``to_frames``).
+
+(Round 6: the projections and convolutions of the null-text loop moved from torch autograd --
+hipBLASLt / MIOpen forward and backward -- to the two frozen-weight functions above.)
 
 Only input gradients exist: the reference optimises the embedding alone (its Adam holds
 ``[uncond_embeddings]``, run_videop2p.py:589), so weight gradients are never consumed; asking for
@@ -157,3 +165,47 @@ class NullTextLoss(torch.autograd.Function):
     def backward(ctx, dloss):
         (grad,) = ctx.saved_tensors
         return grad * dloss.to(grad.dtype), None, None, None, None, None
+
+
+def frozen(*ts) -> bool:
+    """Weights (and bias) that take no gradient: the frozen-weight functions below apply."""
+    return all(t is None or not t.requires_grad for t in ts)
+
+
+class FrozenLinear(torch.autograd.Function):
+    """x @ W^T + b with W, b frozen (the UNet during the null-text optimisation, run_videop2p.py:589
+    optimises the embedding alone): the forward is the inference projection (``ops.linear``: K10 or
+    hipBLASLt by the in-tree table), the backward dx = dy @ W is ``ops.linear`` on a cached W^T."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(weight)
+        return ops.linear(x.contiguous(), weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (w,) = ctx.saved_tensors
+        return ops.linear(dy.contiguous(), ops.transposed_weight(w)), None, None
+
+
+class FrozenConv(torch.autograd.Function):
+    """An InflatedConv3d (``(b f) c h w`` channels-last) with frozen weights: ``run`` is the module's
+    inference convolution (K10 with the fused bias / residual / two-source input, or MIOpen, per the
+    in-tree table); the backward gives dx (split into the two sources when the input is
+    ``cat([x, x2])``) and d(residual) = dy, the input gradient through ``ops.conv2d_input_grad``."""
+
+    @staticmethod
+    def forward(ctx, x, x2, residual, weight, stride, padding, run):
+        ctx.save_for_backward(weight)
+        ctx.geom = (stride, padding, x.shape[1], None if x2 is None else x2.shape[1],
+                    (x.shape[0], x.shape[1] + (0 if x2 is None else x2.shape[1])) + tuple(x.shape[2:]))
+        ctx.has_res = residual is not None
+        return run()
+
+    @staticmethod
+    def backward(ctx, dy):
+        (w,) = ctx.saved_tensors
+        stride, padding, c1, c2, in_shape = ctx.geom
+        dcat = ops.conv2d_input_grad(in_shape, w, dy, stride, padding)
+        dx, dx2 = (dcat, None) if c2 is None else (dcat[:, :c1], dcat[:, c1:])
+        return dx, dx2, (dy if ctx.has_res else None), None, None, None, None

@@ -980,11 +980,60 @@ def linear_add_fused(M: int, K: int, N: int) -> bool:
     return LINEAR.use_k10(M, K, N) and K % 64 == 0 and N % 160 == 0
 
 
+_WT = {}       # (weight storage, version, shape) -> contiguous W^T (frozen weights: the backward's GEMM operand)
+
+
+def transposed_weight(w: torch.Tensor) -> torch.Tensor:
+    """W^T, contiguous, cached while the weight is unchanged (the key holds the weight's version; the
+    entry holds the weight, so its memory cannot be recycled under the key)."""
+    key = (version_key(w), tuple(w.shape), w.dtype)
+    hit = _WT.get(key) if key[0] is not None else None
+    if hit is None:
+        with torch.no_grad():
+            hit = (w, w.detach().t().contiguous())
+        if key[0] is not None:
+            _WT[key] = hit
+    return hit[1]
+
+
+def _kernel_flipped(w: torch.Tensor) -> torch.Tensor:
+    """The transposed convolution's kernel as a forward one: w'[ci, co, i, j] = w[co, ci, k-1-i, k-1-j]
+    (channels-last), cached like ``transposed_weight``."""
+    key = ("conv_t", version_key(w), tuple(w.shape), w.dtype)
+    hit = _WT.get(key) if key[1] is not None else None
+    if hit is None:
+        with torch.no_grad():
+            hit = (w, w.detach().flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last))
+        if key[1] is not None:
+            _WT[key] = hit
+    return hit[1]
+
+
+def conv2d_input_grad(in_shape, weight: torch.Tensor, dy: torch.Tensor, stride: int, padding: int) -> torch.Tensor:
+    """dL/dx of a 2-D convolution with a frozen ``weight``, for the input shape ``in_shape``.  Stride 1
+    with 'same' padding (the 3x3 and 1x1 InflatedConv3d of the resnets, transformers and up blocks) is
+    itself a forward convolution of dy with the flipped, transposed kernel -- run on K10 where it
+    covers the shape (bf16, channel counts); strided ones (Downsample3D) and the rest take MIOpen's
+    backward-data."""
+    k = weight.shape[-1]
+    if stride == 1 and 2 * padding == k - 1 and dy.dtype == torch.bfloat16 and dy.is_cuda:
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        wt = _kernel_flipped(weight)
+        if conv2d_supported(dyc, wt, 1, padding):
+            return conv2d(dyc, wt, None, 1, padding)
+    return torch.nn.grad.conv2d_input(tuple(in_shape), weight, dy, stride, padding)
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
            alpha: Optional[float] = None) -> torch.Tensor:
     """nn.Linear (``alpha``: alpha * (x @ W^T + b), one rounding -- the pre-scaled FrameAttention query).
-    K10's GEMM core where ``LINEAR`` says it is faster for the shape, hipBLASLt elsewhere and for
-    anything that needs a gradient."""
+    K10's GEMM core where ``LINEAR`` says it is faster for the shape, hipBLASLt elsewhere.  Under
+    autograd with frozen weights (the null-text loop) the same dispatch runs forward and backward
+    (``autograd.FrozenLinear``); trainable weights differentiate through torch."""
+    if (alpha is None and torch.is_grad_enabled() and x.requires_grad and x.dtype == torch.bfloat16
+            and not weight.requires_grad and (bias is None or not bias.requires_grad)):
+        from .autograd import FrozenLinear
+        return FrozenLinear.apply(x, weight, bias)
     K, N = x.shape[-1], weight.shape[0]
     M = x.numel() // max(K, 1)
     if linear_k10_ok(x, weight, bias) and LINEAR.use_k10(M, K, N):

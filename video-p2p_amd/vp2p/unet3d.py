@@ -136,6 +136,9 @@ class InflatedConv3d(nn.Conv2d):
 
     def forward(self, x, residual: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None):
         """``x2``: the input is torch.cat([x, x2], dim=1) (1x1 convs read the two parts on K10)."""
+        if (autograd.needs_grad(x, x2, residual) and autograd.frozen(self.weight, self.bias)
+                and x.dtype == torch.bfloat16 and x.is_cuda and type(self) is InflatedConv3d):
+            return self._frozen(x, residual, x2)
         if x2 is not None and autograd.needs_grad(x, x2, self.weight, residual):
             x, x2 = torch.cat([x, x2], dim=1), None
         if autograd.needs_grad(x, self.weight, residual):
@@ -147,6 +150,19 @@ class InflatedConv3d(nn.Conv2d):
                             lambda: super(InflatedConv3d, self).forward(x if x2 is None else torch.cat([x, x2], 1)),
                             x2=x2)
 
+
+    def _frozen(self, x, residual, x2):
+        """Under autograd with frozen weights (the null-text loop): the inference convolution forward
+        and K10's input gradient backward (``autograd.FrozenConv``)."""
+        cl = torch.channels_last
+        x = x.contiguous(memory_format=cl)
+        x2 = None if x2 is None else x2.contiguous(memory_format=cl)
+        residual = None if residual is None else residual.contiguous(memory_format=cl)
+
+        def run():
+            return InflatedConv3d.forward(self, x.detach(), None if residual is None else residual.detach(),
+                                          None if x2 is None else x2.detach())
+        return autograd.FrozenConv.apply(x, x2, residual, self.weight, self.stride[0], self.padding[0], run)
 
     def _padded_k10_fits(self, x) -> bool:
         """conv_in (4 -> 320) and conv_out (320 -> 4): 3x3 'same' bf16 convs whose channel counts
@@ -261,6 +277,8 @@ class GEGLU(nn.Module):
 
     def forward(self, x):
         if autograd.needs_grad(x, self.proj.weight):
+            if type(self.proj) is nn.Linear and not (self.proj._forward_hooks or self.proj._forward_pre_hooks):
+                return autograd.GEGLUFn.apply(ops.linear(x, self.proj.weight, self.proj.bias))
             return autograd.GEGLUFn.apply(self.proj(x))
 
         def unfused():
@@ -304,6 +322,9 @@ class FeedForward(nn.Module):
             if residual is not None:
                 return ops.linear_add(x, out.weight, out.bias, residual)
             return ops.linear(x, out.weight, out.bias)
+        if plain:                 # autograd: ops.linear differentiates (frozen weights: K10 / hipBLASLt)
+            y = ops.linear(x, out.weight, out.bias)
+            return y if residual is None else y + residual
         return out(x) if residual is None else out(x) + residual
 
 
@@ -378,7 +399,7 @@ class Transformer3DModel(nn.Module):
             ok = ops.linear_residual_supported(tok, w_out, res)
             out = fused() if ops.CONV.pick(key, ok, fused, lib) else lib()
             return out.reshape(Bf, H, W, C).permute(0, 3, 1, 2)
-        tok = F.linear(tok, w_out, self.proj_out.bias)
+        tok = ops.linear(tok, w_out, self.proj_out.bias)
         return tok.reshape(Bf, H, W, C).permute(0, 3, 1, 2) + x
 
 
