@@ -1,12 +1,13 @@
 #!/bin/bash
-# K10 A/B: tools/k10_bench.py on the product library and every video-p2p_amd/lib/ab/*.so, two rounds.
+# K10 A/B: tools/k10_bench.py on the product library and every video-p2p_amd/lib/ab/*.so (or lib/$K10AB_DIR),
+# two rounds.
 #   bash tools/gpu/k10_ab.sh TAG
 set -o pipefail
 cd "$(dirname "$0")/../.."
 tag=${1:-k10ab}
 mkdir -p gpurun_out
 for r in 0 1; do
-  for lib in video-p2p_amd/lib/libvp2p_hip.so video-p2p_amd/lib/ab/*.so; do
+  for lib in video-p2p_amd/lib/libvp2p_hip.so video-p2p_amd/lib/${K10AB_DIR:-ab}/*.so; do
     VP2P_LIB=$PWD/$lib timeout -k 10 200 python -u tools/k10_bench.py gpurun_out/$tag.jsonl > gpurun_out/${tag}_last.log 2>&1 || { tail -20 gpurun_out/${tag}_last.log; exit 1; }
   done
 done

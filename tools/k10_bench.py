@@ -32,7 +32,8 @@ g = torch.Generator(device="cuda").manual_seed(0)
 rows = []
 # 3x3 convs: (n, cin, h, cout, stride, residual)
 for n, cin, h, cout, st, res in ((32, 320, 64, 320, 1, True), (32, 640, 64, 320, 1, True), (32, 640, 32, 640, 1, True),
-                                 (32, 1280, 16, 1280, 1, True), (32, 1280, 8, 1280, 1, False),
+                                 (32, 1280, 16, 1280, 1, True), (32, 2560, 16, 1280, 1, False), (32, 1920, 16, 1280, 1, False),
+                                 (32, 1280, 8, 1280, 1, False),
                                  (32, 320, 64, 320, 2, False), (32, 2560, 8, 1280, 1, True)):
     x = torch.randn(n, cin, h, h, device="cuda", generator=g).bfloat16().to(memory_format=torch.channels_last)
     w = (torch.randn(cout, cin, 3, 3, device="cuda", generator=g) * 0.02).bfloat16().to(memory_format=torch.channels_last)
