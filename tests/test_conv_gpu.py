@@ -84,6 +84,41 @@ def test_conv2d_short_tile(n, cin, h, w, cout, k, residual):
     assert _lib.load().vp2p_conv2d_workspace_bytes(ctypes.byref(a)) == 0
 
 
+@pytest.mark.parametrize("n,cin,h,cout,residual,ksplit", [
+    (12, 320, 64, 320, True, 0),        # 3-frame clip res-64: 256 tiles of 192 x 320 (CF 4)
+    (12, 960, 64, 320, False, 0),
+    (13, 320, 63, 320, True, 0),        # ragged last 192-row tile (not the CF 4 grid: the auto plan)
+    (12, 1280, 16, 1280, True, 4),      # res-16, 180 K-steps: 4 slices of 192 128-row tiles
+    (12, 2560, 16, 1280, False, 4),
+])
+def test_conv2d_small_clip_plans(n, cin, h, cout, residual, ksplit):
+    """The 3-frame clip's plans (profiles/r06_k10_plan_sweep.jsonl) vs the fp32 reference; the 192 x 320
+    tile bit-equal to the 128 x 160 one (VP2P_K10_PLAN, same K order), and forced CF 4 on a ragged M."""
+    import ctypes
+    import os
+    from vp2p import ops, _lib
+    _case(n, cin, h, h, cout, 3, 1, residual=residual, seed=9)
+    x = torch.randn(n, cin, h, h, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.02).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b = (torch.randn(cout, device=DEV) * 0.1).to(torch.bfloat16)
+    a, _ = ops._conv_args(x, wt, None, None, None, 1, 1)
+    M = n * h * h
+    assert _lib.load().vp2p_conv2d_workspace_bytes(ctypes.byref(a)) == (ksplit * M * cout * 4 if ksplit else 0)
+    if ksplit:
+        return
+    y = ops.conv2d(x, wt, b, 1, 1)
+    old = os.environ.get("VP2P_K10_PLAN")
+    try:
+        for plan in ("0,1", "4,1"):
+            os.environ["VP2P_K10_PLAN"] = plan
+            assert torch.equal(ops.conv2d(x, wt, b, 1, 1), y), plan
+    finally:
+        if old is None:
+            os.environ.pop("VP2P_K10_PLAN", None)
+        else:
+            os.environ["VP2P_K10_PLAN"] = old
+
+
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv2d_residual(k):
     _case(2, 640, 8, 8, 640, k, 1, residual=True, seed=1)
@@ -238,7 +273,8 @@ def test_attn_temp_residual_on_output_projection(mode):
 
 
 @pytest.mark.parametrize("n,frames,c,h,cout,groups", [(8, 4, 320, 64, 320, 32), (8, 8, 640, 32, 640, 32),
-                                                      (16, 8, 320, 32, 640, 32), (4, 2, 640, 64, 320, 32)])
+                                                      (16, 8, 320, 32, 640, 32), (4, 2, 640, 64, 320, 32),
+                                                      (12, 3, 320, 64, 320, 32)])     # the 192 x 320 tile
 def test_conv2d_gn_stats(n, frames, c, h, cout, groups):
     """conv1 + temb with norm2's statistics left by K10's epilogue (ops.conv2d_gn): the output equals
     the separate conv + add bit for bit (same tile, same two roundings), and the GroupNorm applied

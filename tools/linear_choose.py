@@ -2,9 +2,11 @@
 K10 picks itself) against hipBLASLt (``F.linear``) over a range of row counts M, and write the
 ``linear_rules`` of ``miopen_db/kernel_choices.json`` that ``vp2p.ops.LinearRule`` reads: per (K, N),
 the runs of consecutive measured M over which K10 is faster by > 2 % (open-ended at the measured
-extremes).  ``--from OLD.jsonl`` recomputes the rules from a committed measurement.
+extremes).  ``--from OLD.jsonl`` recomputes the rules from a committed measurement; with ``--ms M1,M2,..``
+as well, only those row counts are measured and merged into OLD's rows (the other M keep OLD's
+timings, so decisions at OLD's measured M do not move).
 
-Run on the MI355X:  python tools/linear_choose.py OUT.jsonl [--write]"""
+Run on the MI355X:  python tools/linear_choose.py OUT.jsonl [--write] [--from OLD.jsonl --ms 768,3072]"""
 import json
 import os
 import sys
@@ -45,25 +47,30 @@ def main():
     out = sys.argv[1]
     write = "--write" in sys.argv
     rows = []
+    ms = None
+    if "--ms" in sys.argv:
+        ms = tuple(int(m) for m in sys.argv[sys.argv.index("--ms") + 1].split(","))
     if "--from" in sys.argv:
         with open(sys.argv[sys.argv.index("--from") + 1]) as fh:
             rows = [json.loads(line) for line in fh]
-    else:
-        rows = measure()
+    if ms is not None or not rows:
+        new = measure(ms or MS)
+        keys = {(r["M"], r["K"], r["N"]) for r in new}
+        rows = [r for r in rows if (r["M"], r["K"], r["N"]) not in keys] + new
         with open(out, "w") as fh:
             for r in rows:
                 fh.write(json.dumps(r) + "\n")
     write_rules(rows, write)
 
 
-def measure():
+def measure(ms):
     g = torch.Generator(device="cuda").manual_seed(0)
     rows = []
     torch.set_grad_enabled(False)
     for K, N in PAIRS:
         w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
         b = (torch.randn(N, device="cuda", generator=g) * 0.1).bfloat16()
-        for M in MS:
+        for M in ms:
             if M * max(K, N) * 2 > 2 ** 31:
                 continue
             x = torch.randn(M, K, device="cuda", generator=g).bfloat16()

@@ -40,6 +40,7 @@
 // (profiles/r02_conv_up_bench.jsonl).  Tried and
 // dropped: register staging (~800), 256-row tiles with three LDS stages and a counted-vmcnt barrier
 // span (-5 %), one wave per 32 rows x 160 columns on 32x32x16 MFMAs (-9 %: every wave reads all of B).
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <type_traits>
@@ -104,6 +105,9 @@ constexpr int GBM = 128, NW = 4;                               // the split-K / 
 //     byte read and per barrier of 0 / 1 (Cout % 320 == 0; the epilogue runs in two 128-row passes);
 //  3: 64 x 160 "short", 4 waves (2 x 2 of 32 x 80), two stages: the small-clip shapes whose 128-row
 //     grid would leave CUs idle (1-2 frame edits), one pass where 0 needed a split-K second pass;
+//  4: 192 x 320 "mid", 8 waves (2 x 4 of 96 x 80), two stages (2 x 64 KB), one workgroup per CU:
+//     the grids whose 192-row tiles come out at whole waves of 256 where 0 / 2 leave a part-filled
+//     last wave (the 3-frame clip's 64x64 convs: M 49152, 256 tiles, against 768 of 0 = 3 per CU);
 // All: the same per-output K order and MFMA sequence (one 16x16x32 MFMA per 32 channels), so
 // bit-equal results.
 template <int TBM_, int TBN_, int WTM_, int NST_, int KB_ = 64, int WTN_ = 5> struct GTile {
@@ -134,6 +138,7 @@ template <> struct GCfg<0> : GTile<128, 160, 4, 2> {};
 template <> struct GCfg<1> : GTile<256, 160, 4, 3> {};
 template <> struct GCfg<2> : GTile<256, 320, 8, 2> {};
 template <> struct GCfg<3> : GTile<64, 160, 2, 2> {};
+template <> struct GCfg<4> : GTile<192, 320, 6, 2> {};
 // The GEGLU epilogue's form of each tile: the same block, threads, stages and LDS, with every wave
 // 160 columns wide (10 16-column tiles = 5 (value, gate) pairs of the same 16 channels: the weights
 // come interleaved per 16 as [16 value rows | 16 gate rows]), so a lane holds a channel's value and
@@ -723,6 +728,11 @@ __global__ __launch_bounds__(256, 2) void conv_kernel_s(const vp2p_conv_args a) 
   conv_tile<KS, EPI, AM, 3>(a);
 }
 
+template <int KS, int EPI = 0, int AM = 1>
+__global__ __launch_bounds__(512, 1) void conv_kernel_m(const vp2p_conv_args a) {
+  conv_tile<KS, EPI, AM, 4>(a);
+}
+
 // ------------------------------------------------------------------------------------------------
 // K10s: the K = 320 1x1 GEMMs of the 64x64-latent transformer blocks as a persistent stream --
 // proj_in, to_q, to_out, proj_out, attn_temp's to_out (N = 320: y = x W^T (+ bias) (* alpha)
@@ -994,6 +1004,9 @@ template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 2> {
 template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 3> {
   static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_s<KS, EPI, AM>); }
 };
+template <int KS, int EPI, int AM> struct ConvKernel<KS, EPI, AM, 4> {
+  static const void* fn() { return reinterpret_cast<const void*>(&conv_kernel_m<KS, EPI, AM>); }
+};
 
 // split-K second pass: y = round(round(sum_s ws[s] + bias) + residual), the one-pass roundings
 __global__ __launch_bounds__(256) void conv_splitk_reduce(const vp2p_conv_args a) {
@@ -1041,8 +1054,10 @@ static int launch_g1(const vp2p_conv_args& a, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL((conv_kernel_b<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   else if constexpr (CF == 2)
     hipLaunchKernelGGL((conv_kernel_w<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
-  else
+  else if constexpr (CF == 3)
     hipLaunchKernelGGL((conv_kernel_s<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
+  else
+    hipLaunchKernelGGL((conv_kernel_m<KS, EPI, AM>), grid, dim3(Cfg::NT), Cfg::LDS, s, a);
   return hipGetLastError() == hipSuccess ? VP2P_OK : VP2P_E_LAUNCH;
 }
 
@@ -1087,11 +1102,30 @@ static int pick_tile(const vp2p_conv_args* a, int64_t M) {
 // them: >= 384 tiles, or >= 256 on short K (<= 48 K-steps; longer K keeps split-K, which measured
 // faster there).  Small-clip shapes, profiles/r04_k10_short_tile.jsonl: 1-frame res-64 3x3
 // 56.2 -> 43.4 us, 2-frame res-32 3x3 (320 -> 640) 50.5 -> 35.2 us, M 4096 K 640 N 640 14.4 -> 10.0 us.
+// Not for a long-K 3x3 (> 96 steps) whose 64-row grid still ends in a part-filled wave: split-K over
+// 128-row tiles measured faster there (profiles/r06_k10_plan_sweep.jsonl, the 3-frame clip's 16x16
+// convs, M 3072 N 1280 K 1280 / 1920 / 2560 x 9: 114.7 / 161.1 / 224.2 -> 101.2 / 135.9 / 171.6 us at
+// 4 slices), except on the upsampling form, which split-K would give up.
 static bool short_tile(const vp2p_conv_args* a, int64_t M) {
   const int64_t tiles = (M + GBM - 1) / GBM * (a->cout / BN);
   const int64_t tiles_s = (M + 63) / 64 * (a->cout / BN);
   const int nsteps = a->kernel * a->kernel * (a->cin / BK);
+  if (a->kernel == 3 && nsteps > 96 && tiles_s < 512 && !a->upsample) return false;
+  // short-K projections (<= 30 K-steps) on however few tiles: one pass beat the 2-slice split there
+  // (M 1024 / 768 / 256, K 1280, N 1280: 19.0 / 17.9 / 14.8 -> 13.1 / 12.9 / 12.3 us, r06 sweep)
+  if (a->kernel == 1 && nsteps <= 30 && tiles < 384) return true;
   return tiles < 384 && (tiles_s >= 384 || (tiles_s >= 256 && nsteps <= 48));
+}
+
+// The 192 x 320 tile (CF 4) for a plain conv / projection whose 192-row grid is one or two whole waves
+// of 256 where the others end part-filled or run 3+ tiles per CU (profiles/r06_k10_plan_sweep.jsonl,
+// the 3-frame clip: 64x64 3x3 N 320 K 320 / 640 / 960 x 9: 85.0 / 156.4 / 224.9 -> 73.1 / 132.5 /
+// 193.6 us; the Upsample3D convs 64x64 N 640 296.2 -> 270.7, 32x32 N 1280 301.3 -> 266.3;
+// r06_k10_plan_linear.jsonl: M 49152 N 320 K 640 / 960 / 1280 30.7 / 40.3 / 59.0 -> 26.0 / 33.2 / 40.2)
+static bool mid_tile(const vp2p_conv_args* a, int64_t M) {
+  if (a->epilogue != VP2P_CONV_EPI_NONE || a->cout % 320) return false;
+  const int64_t tiles = (M + 191) / 192 * (a->cout / 320);
+  return tiles <= 512 && wave_fill(tiles, 256) >= 0.95;
 }
 
 // K-split for this shape: 1 unless the grid would leave most CUs idle (the 8x8-latent convs)
@@ -1105,11 +1139,58 @@ static int pick_ksplit(const vp2p_conv_args* a) {
   // at most 8 slices, 16 where 8 would leave half the CUs without a workgroup (<= 16 tiles: the
   // 8x8-latent convs of a 1-frame clip; profiles/r04_k10_ksplit16.jsonl: M 256 K 2560*9 N 1280
   // 46.1 -> 35.0 us, K 1280*9 29.1 -> 25.4 us; 16 slices of the 32-tile grids measured slower)
-  const int cap = tiles <= 16 ? 16 : 8;
-  int k = (int)((512 + tiles - 1) / tiles);
-  if (k > cap) k = cap;
-  while (k > 1 && nsteps / k < 8) --k;                          // keep >= 8 steps per slice
+  int kmax = tiles <= 16 ? 16 : 8;
+  if (nsteps / 8 < kmax) kmax = nsteps / 8;                      // keep >= 8 steps per slice
+  if (kmax < 2) return 1;
+  int k0 = (int)((512 + tiles - 1) / tiles);
+  if (k0 > kmax) k0 = kmax;
+  // of k0 - 1, k0, k0 + 1 the one whose grid best fills its last wave of 512 (ties: more slices):
+  // 192 tiles take 4 slices (768 = 1.5 waves), not 3 (576: a 64-workgroup second wave), measured
+  // 101.2 / 135.9 / 171.6 vs 117.0 / 160.9 / 206.4 us (profiles/r06_k10_plan_sweep.jsonl)
+  int k = k0;
+  double best = -1.0;
+  for (int c = k0 - 1; c <= k0 + 1; ++c) {
+    if (c < 2 || c > kmax) continue;
+    const double f = wave_fill(tiles * c, 512);
+    if (f >= best) { best = f; k = c; }
+  }
   return k;
+}
+
+// The launch plan of a shape: tile configuration cf and K-split k (1: one pass).
+struct Plan {
+  int cf, k;
+};
+
+static bool plan_valid(const vp2p_conv_args* a, int cf, int k) {
+  if (cf < 0 || cf > 4 || k < 1 || k > 16) return false;
+  if ((cf == 2 || cf == 4) && a->cout % 320) return false;
+  if (cf == 4 && a->epilogue != VP2P_CONV_EPI_NONE) return false;
+  if (k > 1 && (a->epilogue != VP2P_CONV_EPI_NONE || (cf != 0 && cf != 3))) return false;
+  return a->kernel * a->kernel * (a->cin / BK) >= k;
+}
+
+// VP2P_K10_PLAN="CF,K" (tools/k10_plan_sweep.py: A/B only) forces both wherever they are valid for the
+// shape; read on every call, so a sweep can change it between launches
+static Plan plan_of(const vp2p_conv_args* a) {
+  const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
+  Plan p{0, pick_ksplit(a)};
+  if (p.k == 1) p.cf = short_tile(a, M) ? 3 : mid_tile(a, M) ? 4 : pick_tile(a, M);
+  if (const char* e = getenv("VP2P_K10_PLAN")) {
+    int cf = -1, k = 0;
+    if (sscanf(e, "%d,%d", &cf, &k) == 2 && plan_valid(a, cf, k)) p = Plan{cf, k};
+  }
+  return p;
+}
+
+static void tile_dims(int cf, int* tbm, int* tbn, int* nt) {
+  switch (cf) {
+    case 1: *tbm = GCfg<1>::TBM; *tbn = GCfg<1>::TBN; *nt = GCfg<1>::NT; break;
+    case 2: *tbm = GCfg<2>::TBM; *tbn = GCfg<2>::TBN; *nt = GCfg<2>::NT; break;
+    case 3: *tbm = GCfg<3>::TBM; *tbn = GCfg<3>::TBN; *nt = GCfg<3>::NT; break;
+    case 4: *tbm = GCfg<4>::TBM; *tbn = GCfg<4>::TBN; *nt = GCfg<4>::NT; break;
+    default: *tbm = GCfg<0>::TBM; *tbn = GCfg<0>::TBN; *nt = GCfg<0>::NT; break;
+  }
 }
 
 }  // namespace conv
@@ -1142,30 +1223,16 @@ extern "C" int vp2p_conv2d_supported(const vp2p_conv_args* a) {
   return 1;
 }
 
-namespace vp2p {
-namespace conv {
-// (TBM, TBN, threads) of the one-pass tile vp2p_conv2d_fwd picks for this shape (CF as in the launch)
-static void one_pass_tile(const vp2p_conv_args* a, int64_t M, int* tbm, int* tbn, int* nt) {
-  int cf = short_tile(a, M) ? 3 : pick_tile(a, M);
-  switch (cf) {
-    case 1: *tbm = GCfg<1>::TBM; *tbn = GCfg<1>::TBN; *nt = GCfg<1>::NT; break;
-    case 2: *tbm = GCfg<2>::TBM; *tbn = GCfg<2>::TBN; *nt = GCfg<2>::NT; break;
-    case 3: *tbm = GCfg<3>::TBM; *tbn = GCfg<3>::TBN; *nt = GCfg<3>::NT; break;
-    default: *tbm = GCfg<0>::TBM; *tbn = GCfg<0>::TBN; *nt = GCfg<0>::NT; break;
-  }
-}
-}  // namespace conv
-}  // namespace vp2p
-
 extern "C" int32_t vp2p_conv2d_gn_parts(const vp2p_conv_args* a) {
   if (!a || !vp2p_conv2d_supported(a)) return 0;
   if (a->epilogue != VP2P_CONV_EPI_NONE || (a->alpha != 0.f && a->alpha != 1.f)) return 0;
-  if (conv::pick_ksplit(a) > 1) return 0;                       // statistics in the one-pass epilogue only
+  const conv::Plan pl = conv::plan_of(a);
+  if (pl.k > 1) return 0;                                       // statistics in the one-pass epilogue only
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   if (a->gn_groups <= 0 || a->cout % a->gn_groups || a->gn_rows <= 0 || M % a->gn_rows) return 0;
   const int cg = a->cout / a->gn_groups;
   int tbm, tbn, nt;
-  conv::one_pass_tile(a, M, &tbm, &tbn, &nt);
+  conv::tile_dims(pl.cf, &tbm, &tbn, &nt);
   if (cg % 2 || tbn % cg || a->gn_rows % tbm) return 0;
   const int gt = tbn / cg;
   if (nt % gt) return 0;
@@ -1176,7 +1243,7 @@ extern "C" int32_t vp2p_conv2d_gn_parts(const vp2p_conv_args* a) {
 
 extern "C" int64_t vp2p_conv2d_workspace_bytes(const vp2p_conv_args* a) {
   if (!a || !vp2p_conv2d_supported(a)) return 0;
-  const int k = conv::pick_ksplit(a);
+  const int k = conv::plan_of(a).k;
   return k > 1 ? (int64_t)k * a->batch * a->out_h * a->out_w * a->cout * 4 : 0;
 }
 
@@ -1191,9 +1258,15 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   if (M * a->cout > ((int64_t)1 << 40)) return VP2P_E_SHAPE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t tiles = (M + conv::GBM - 1) / conv::GBM * (a->cout / conv::BN);
-  int k = conv::pick_ksplit(a);
-  if (k > 1 && !a->workspace) k = 1;                    // no workspace given: one pass
+  conv::Plan pl = conv::plan_of(a);
+  if (pl.k > 1 && !a->workspace) {                      // no workspace given: one pass
+    pl.k = 1;
+    pl.cf = conv::short_tile(a, M) ? 3 : conv::mid_tile(a, M) ? 4 : conv::pick_tile(a, M);
+  }
+  const int k = pl.k;
+  int tbm, tbn, nt_;
+  conv::tile_dims(pl.cf, &tbm, &tbn, &nt_);
+  const int64_t tiles = (M + tbm - 1) / tbm * (a->cout / tbn);
   // addressing: 32-bit buffer offsets when the stored input is below 2^31 bytes (the upsampling
   // form for the one-pass 3x3 kernel), 64-bit pointers otherwise
   const int64_t in_bytes = (int64_t)a->batch * (a->in_h >> a->upsample) * (a->in_w >> a->upsample) * a->cin * 2;
@@ -1221,22 +1294,24 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
   } else if (k > 1) {
     vp2p_conv_args b = *a;
     b.ksplit = k;
-    rc = a->kernel == 3 ? conv::launch_g<3, 2>(b, grid, fast, s) : conv::launch_g<1, 2>(b, grid, fast, s);
+    if (pl.cf == 3)
+      rc = a->kernel == 3 ? conv::launch_g<3, 2, 3>(b, grid, fast, s) : conv::launch_g<1, 2, 3>(b, grid, fast, s);
+    else
+      rc = a->kernel == 3 ? conv::launch_g<3, 2>(b, grid, fast, s) : conv::launch_g<1, 2>(b, grid, fast, s);
     if (rc != VP2P_OK) return rc;
     const int64_t n = M * (a->cout / 8);
     hipLaunchKernelGGL(conv::conv_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
-  } else if (conv::short_tile(a, M)) {
-    const dim3 gs((unsigned)((M + 63) / 64 * (a->cout / conv::BN)));
-    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 3>(*a, gs, fast, s);
-    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 3>(*a, gs, fast, s) : conv::launch_g<1, 0, 3>(*a, gs, fast, s);
-  } else if (const int cf = conv::pick_tile(a, M); cf == 1) {
-    const dim3 gb((unsigned)((M + 255) / 256 * (a->cout / conv::BN)));
-    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 1>(*a, gb, fast, s);
-    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 1>(*a, gb, fast, s) : conv::launch_g<1, 0, 1>(*a, gb, fast, s);
-  } else if (cf == 2) {
-    const dim3 gw((unsigned)((M + 255) / 256 * (a->cout / 320)));
-    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 2>(*a, gw, fast, s);
-    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 2>(*a, gw, fast, s) : conv::launch_g<1, 0, 2>(*a, gw, fast, s);
+  } else if (pl.cf == 3) {
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 3>(*a, grid, fast, s);
+    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 3>(*a, grid, fast, s) : conv::launch_g<1, 0, 3>(*a, grid, fast, s);
+  } else if (pl.cf == 1) {
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 1>(*a, grid, fast, s);
+    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 1>(*a, grid, fast, s) : conv::launch_g<1, 0, 1>(*a, grid, fast, s);
+  } else if (pl.cf == 2) {
+    if (a->epilogue == VP2P_CONV_EPI_GEGLU) rc = conv::launch_g<1, 1, 2>(*a, grid, fast, s);
+    else rc = a->kernel == 3 ? conv::launch_g<3, 0, 2>(*a, grid, fast, s) : conv::launch_g<1, 0, 2>(*a, grid, fast, s);
+  } else if (pl.cf == 4) {     // plain epilogue only (plan_valid)
+    rc = a->kernel == 3 ? conv::launch_g<3, 0, 4>(*a, grid, fast, s) : conv::launch_g<1, 0, 4>(*a, grid, fast, s);
   } else if (a->epilogue == VP2P_CONV_EPI_GEGLU) {
     rc = conv::launch_g<1, 1>(*a, grid, fast, s);
   } else {
