@@ -88,7 +88,7 @@ def test_conv2d_short_tile(n, cin, h, w, cout, k, residual):
     (12, 320, 64, 320, True, 0),        # 3-frame clip res-64: 256 tiles of 192 x 320 (CF 4)
     (12, 960, 64, 320, False, 0),
     (13, 320, 63, 320, True, 0),        # ragged last 192-row tile (not the CF 4 grid: the auto plan)
-    (12, 1280, 16, 1280, True, 4),      # res-16, 180 K-steps: 4 slices of 192 128-row tiles
+    (12, 1280, 16, 1280, True, 4),      # res-16, 180 K-steps: 4 slices of 64 192 x 320 tiles
     (12, 2560, 16, 1280, False, 4),
 ])
 def test_conv2d_small_clip_plans(n, cin, h, cout, residual, ksplit):
@@ -187,7 +187,8 @@ def test_linear_geglu(M, K, inner):
     assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("n,cin,h,w,cout", [(2, 1280, 8, 8, 1280), (3, 640, 5, 7, 640), (32, 640, 32, 32, 320)])
+@pytest.mark.parametrize("n,cin,h,w,cout", [(2, 1280, 8, 8, 1280), (3, 640, 5, 7, 640), (32, 640, 32, 32, 320),
+                                          (12, 1280, 8, 8, 1280)])   # 3-frame clip: 4 slices of 192 x 320
 def test_conv2d_fused_upsample(n, cin, h, w, cout):
     """K10 reading a x2 nearest upsample on the fly == F.interpolate then the conv (fp32 reference)."""
     from vp2p import ops

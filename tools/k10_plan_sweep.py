@@ -14,7 +14,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "video-p2p_amd"))
 from vp2p import ops  # noqa: E402
 
-PLANS = ["auto"] + [f"{cf},1" for cf in range(5)] + [f"{cf},{k}" for cf in (0, 3) for k in (2, 3, 4, 6, 8)]
+PLANS = ["auto"] + [f"{cf},1" for cf in range(5)] + [f"{cf},{k}" for cf in (0, 3, 4) for k in (2, 3, 4, 6, 8)]
 # (cin, h, cout, stride, upsample): resnet convs, Downsample2D (stride 2), Upsample3D (x2 nearest on the fly)
 SHAPES = [(320, 64, 320, 1, 0), (640, 64, 320, 1, 0), (960, 64, 320, 1, 0),
           (320, 32, 640, 1, 0), (640, 32, 640, 1, 0), (1280, 32, 640, 1, 0), (960, 32, 640, 1, 0),

@@ -1157,6 +1157,21 @@ static int pick_ksplit(const vp2p_conv_args* a) {
   return k;
 }
 
+// K-split on the 192 x 320 tile where its slices make exactly one wave of 256 workgroups (>= 32 K-steps
+// a slice) in the small-M regime (< 384 128 x 160 tiles): the 3-frame clip's 16x16 3x3 convs, M 3072
+// N 1280, 4 slices of 64 tiles -- K 1280 / 1920 / 2560 x 9 98.7 / 132.1 / 170.1 -> 91.9 / 122.9 / 154.2 us,
+// and the Upsample3D conv there (otherwise the one-pass short tile) 113.8 -> 98.0
+// (profiles/r06_k10_plan_split4.jsonl)
+static int mid_split(const vp2p_conv_args* a, int64_t M) {
+  if (a->kernel != 3 || a->epilogue != VP2P_CONV_EPI_NONE || a->cout % 320) return 0;
+  if ((M + GBM - 1) / GBM * (a->cout / BN) >= 384) return 0;
+  const int64_t tiles = (M + 191) / 192 * (a->cout / 320);
+  const int nsteps = a->kernel * a->kernel * (a->cin / BK);
+  for (int k = 2; k <= 8; ++k)
+    if (tiles * k == 256 && nsteps / k >= 32) return k;
+  return 0;
+}
+
 // The launch plan of a shape: tile configuration cf and K-split k (1: one pass).
 struct Plan {
   int cf, k;
@@ -1166,7 +1181,7 @@ static bool plan_valid(const vp2p_conv_args* a, int cf, int k) {
   if (cf < 0 || cf > 4 || k < 1 || k > 16) return false;
   if ((cf == 2 || cf == 4) && a->cout % 320) return false;
   if (cf == 4 && a->epilogue != VP2P_CONV_EPI_NONE) return false;
-  if (k > 1 && (a->epilogue != VP2P_CONV_EPI_NONE || (cf != 0 && cf != 3))) return false;
+  if (k > 1 && (a->epilogue != VP2P_CONV_EPI_NONE || (cf != 0 && cf != 3 && cf != 4))) return false;
   return a->kernel * a->kernel * (a->cin / BK) >= k;
 }
 
@@ -1175,7 +1190,8 @@ static bool plan_valid(const vp2p_conv_args* a, int cf, int k) {
 static Plan plan_of(const vp2p_conv_args* a) {
   const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
   Plan p{0, pick_ksplit(a)};
-  if (p.k == 1) p.cf = short_tile(a, M) ? 3 : mid_tile(a, M) ? 4 : pick_tile(a, M);
+  if (const int km = mid_split(a, M)) p = Plan{4, km};
+  else if (p.k == 1) p.cf = short_tile(a, M) ? 3 : mid_tile(a, M) ? 4 : pick_tile(a, M);
   if (const char* e = getenv("VP2P_K10_PLAN")) {
     int cf = -1, k = 0;
     if (sscanf(e, "%d,%d", &cf, &k) == 2 && plan_valid(a, cf, k)) p = Plan{cf, k};
@@ -1296,6 +1312,8 @@ extern "C" int vp2p_conv2d_fwd(const vp2p_conv_args* a, void* stream) {
     b.ksplit = k;
     if (pl.cf == 3)
       rc = a->kernel == 3 ? conv::launch_g<3, 2, 3>(b, grid, fast, s) : conv::launch_g<1, 2, 3>(b, grid, fast, s);
+    else if (pl.cf == 4)
+      rc = a->kernel == 3 ? conv::launch_g<3, 2, 4>(b, grid, fast, s) : conv::launch_g<1, 2, 4>(b, grid, fast, s);
     else
       rc = a->kernel == 3 ? conv::launch_g<3, 2>(b, grid, fast, s) : conv::launch_g<1, 2>(b, grid, fast, s);
     if (rc != VP2P_OK) return rc;
