@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VP2P_ABI_VERSION 15
+#define VP2P_ABI_VERSION 16
 
 enum vp2p_status {
   VP2P_OK = 0,
@@ -394,6 +394,10 @@ int vp2p_conv2d_supported(const vp2p_conv_args* args);
 int32_t vp2p_conv2d_gn_parts(const vp2p_conv_args* args);
 /* Workspace the shape wants for split-K (small-M shapes: fewer tiles than CUs); 0 = none. */
 int64_t vp2p_conv2d_workspace_bytes(const vp2p_conv_args* args);
+/* (since ABI 16) The launch plan vp2p_conv2d_fwd takes for this shape (given a workspace where it wants
+ * one): *tile = 0 128x160, 1 256x160, 2 256x320, 3 64x160, 4 192x320, or 5 the K = 320 stream (K10s);
+ * *ksplit = K slices (1 = one pass).  Host logic only; VP2P_OK or VP2P_E_SHAPE (unsupported). */
+int vp2p_conv2d_plan(const vp2p_conv_args* args, int32_t* tile, int32_t* ksplit);
 int vp2p_conv2d_fwd(const vp2p_conv_args* args, void* stream);
 
 /* ---- introspection ---------------------------------------------------------------------------- */

@@ -141,6 +141,51 @@ def test_conv_gn_parts_host():
     assert lib.vp2p_conv2d_supported(ctypes.byref(c)) == 0
 
 
+def test_conv_plan_host(monkeypatch):
+    """vp2p_conv2d_plan (ABI 16): the K10 launch plan per shape -- the measured rules of DESIGN §4
+    (profiles/r06_k10_plan_*.jsonl, r06_small_clip_*): 8-frame edit on the wide tile, the 3-frame clip's
+    64x64 convs on 192 x 320, its 16x16 long-K convs on 4 slices of 192 x 320, the 1-frame clip's on
+    the short tile (host logic, no GPU)."""
+    import ctypes
+    from vp2p import _lib
+    lib = _lib.load()
+
+    def plan(n, h, cin, cout, k=3, up=0, epi=_lib.CONV_EPI_NONE):
+        a = _lib.ConvArgs(None, None, None, None, None, n, h, h, cin, cout, h, h, k, 1, (k - 1) // 2, _lib.BF16,
+                          epi)
+        a.upsample = up
+        t, ks = ctypes.c_int32(-1), ctypes.c_int32(-1)
+        assert lib.vp2p_conv2d_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(ks)) == 0
+        return t.value, ks.value
+
+    monkeypatch.delenv("VP2P_K10_PLAN", raising=False)
+    assert plan(32, 64, 320, 320) == (2, 1)           # 8 frames, 64x64: 512 wide tiles
+    assert plan(32, 8, 1280, 1280) == (0, 4)          # 8 frames, 8x8: 128 tiles x 4 slices
+    assert plan(12, 64, 320, 320) == (4, 1)           # 3 frames, 64x64: 256 tiles of 192 x 320
+    assert plan(12, 64, 960, 320) == (4, 1)
+    assert plan(12, 32, 640, 640) == (0, 1)           # 3 frames, 32x32: 384 tiles of 128 x 160
+    assert plan(12, 16, 1280, 1280) == (4, 4)         # 3 frames, 16x16, 180 K-steps: 64 tiles x 4
+    assert plan(12, 16, 2560, 1280) == (4, 4)
+    assert plan(12, 16, 640, 1280) == (3, 1)          # 90 K-steps: one pass on the short tile
+    assert plan(12, 16, 1280, 1280, up=1) == (4, 4)   # the Upsample3D conv there
+    assert plan(4, 64, 320, 320) == (3, 1)            # 1 frame, 64x64: 512 short tiles
+    assert plan(12, 64, 320, 320, k=1) == (5, 1)      # K = 320 projection: the K10s stream
+    a = _lib.ConvArgs(None, None, None, None, None, 768, 1, 1, 1280, 1280, 1, 1, 1, 1, 0, _lib.BF16,
+                      _lib.CONV_EPI_NONE)
+    t, ks = ctypes.c_int32(-1), ctypes.c_int32(-1)
+    assert lib.vp2p_conv2d_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(ks)) == 0
+    assert (t.value, ks.value) == (3, 1)               # short-K projection, 48 tiles: one pass, not split
+    monkeypatch.setenv("VP2P_K10_PLAN", "0,1")         # the A/B override, where valid
+    assert plan(12, 64, 320, 320) == (0, 1)
+    monkeypatch.delenv("VP2P_K10_PLAN")
+    geglu = plan(32, 16, 1280, 10240, k=1, epi=_lib.CONV_EPI_GEGLU)
+    monkeypatch.setenv("VP2P_K10_PLAN", "4,2")         # invalid for the GEGLU epilogue: ignored
+    assert plan(32, 16, 1280, 10240, k=1, epi=_lib.CONV_EPI_GEGLU) == geglu
+    monkeypatch.delenv("VP2P_K10_PLAN")
+    a.cin = 100                                        # unsupported shape
+    assert lib.vp2p_conv2d_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(ks)) == -4
+
+
 def test_geglu_interleave_layout():
     """K10's GEGLU weight order: per 32 rows, 16 value rows then the matching 16 gate rows."""
     import torch

@@ -1257,6 +1257,21 @@ extern "C" int32_t vp2p_conv2d_gn_parts(const vp2p_conv_args* a) {
   return a->gn_rows / tbm;
 }
 
+extern "C" int vp2p_conv2d_plan(const vp2p_conv_args* a, int32_t* tile, int32_t* ksplit) {
+  if (!a || !tile || !ksplit) return VP2P_E_ARG;
+  if (!vp2p_conv2d_supported(a)) return VP2P_E_SHAPE;
+  const int64_t M = (int64_t)a->batch * a->out_h * a->out_w;
+  if (conv::skinny_kind(a, M)) {
+    *tile = 5;
+    *ksplit = 1;
+    return VP2P_OK;
+  }
+  const conv::Plan pl = conv::plan_of(a);
+  *tile = pl.cf;
+  *ksplit = pl.k;
+  return VP2P_OK;
+}
+
 extern "C" int64_t vp2p_conv2d_workspace_bytes(const vp2p_conv_args* a) {
   if (!a || !vp2p_conv2d_supported(a)) return 0;
   const int k = conv::plan_of(a).k;

@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP2P_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libvp2p_hip.so"))
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 F32, BF16 = 0, 1
 EDIT_NONE, EDIT_REPLACE, EDIT_REFINE = 0, 1, 2
 CONV_EPI_NONE, CONV_EPI_GEGLU = 0, 1
@@ -31,7 +31,7 @@ EXPORTS = ("vp2p_frame_attn_fwd", "vp2p_cross_kv_workspace_bytes", "vp2p_cross_k
            "vp2p_add_layer_norm_fwd", "vp2p_conv2d_workspace_bytes", "vp2p_group_norm_finalize",
            "vp2p_group_norm_apply_stats", "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged",
            "vp2p_group_norm_finalize_parts", "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts",
-           "vp2p_group_norm_apply_parts")
+           "vp2p_group_norm_apply_parts", "vp2p_conv2d_plan")
 
 
 class GroupNormArgs(ctypes.Structure):
@@ -180,6 +180,7 @@ def load(path: str = None):
     lib.vp2p_conv2d_fwd.argtypes = [POINTER(ConvArgs), c_void_p]
     lib.vp2p_conv2d_workspace_bytes.argtypes = [POINTER(ConvArgs)]
     lib.vp2p_conv2d_gn_parts.argtypes = [POINTER(ConvArgs)]
+    lib.vp2p_conv2d_plan.argtypes = [POINTER(ConvArgs), POINTER(c_int32), POINTER(c_int32)]
     lib.vp2p_group_norm_finalize_parts.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p]
     lib.vp2p_group_norm_merge_parts.argtypes = [gn, c_void_p, c_int32, c_void_p, c_void_p]
     lib.vp2p_group_norm_apply_parts.argtypes = [gn, c_void_p, c_int32, c_void_p]
@@ -194,7 +195,8 @@ def load(path: str = None):
                  "vp2p_nulltext_loss_partials", "vp2p_conv2d_supported", "vp2p_conv2d_fwd",
                  "vp2p_add_layer_norm_fwd", "vp2p_group_norm_finalize", "vp2p_group_norm_apply_stats",
                  "vp2p_group_norm_merge", "vp2p_group_norm_finalize_merged", "vp2p_group_norm_finalize_parts",
-                 "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts", "vp2p_group_norm_apply_parts"):
+                 "vp2p_group_norm_merge_parts", "vp2p_conv2d_gn_parts", "vp2p_group_norm_apply_parts",
+                 "vp2p_conv2d_plan"):
         getattr(lib, name).restype = c_int32
     if lib.vp2p_abi_version() != ABI_VERSION:
         raise Vp2pError(f"{p}: ABI version {lib.vp2p_abi_version()} != {ABI_VERSION}; rebuild")
