@@ -4,7 +4,7 @@
 # residual / plain, the N = 2560 GEGLU), each as its own target (tools/conv_only.py /
 # tools/gemm_only.py) in five passes: A/B/C (wave-cycle split, MFMA busy, LDS), F (FETCH_SIZE),
 # W (WRITE_SIZE).  Summaries -> gpurun_out/k10pmc/summary.txt, traffic -> gpurun_out/k10pmc/*.json
-#   bash tools/gpu/k10_pmc.sh
+#   [K10PMC_SET=small] bash tools/gpu/k10_pmc.sh
 set -o pipefail
 cd "$(dirname "$0")/../.."
 out=gpurun_out/k10pmc
@@ -27,6 +27,15 @@ run() {  # name kernel_substr alg_bytes cmd...
   echo "$name ok"
 }
 rm -f $out/summary.txt
+if [ "$K10PMC_SET" = small ]; then   # the 3-frame clip's 64^2 convs: the 192 x 320 tile vs 128 x 160 (VP2P_K10_PLAN=0,1)
+  mkdir -p $out/m320 $out/g320 $out/m960 $out/g960
+  run m320 "conv_kernel_m<3" $((2 * (12*4096*320*3 + 320*320*9))) python3 tools/conv_only.py 12 320 64 320 5 &&
+  VP2P_K10_PLAN=0,1 run g320 "conv_kernel_g<3" $((2 * (12*4096*320*3 + 320*320*9))) python3 tools/conv_only.py 12 320 64 320 5 &&
+  run m960 "conv_kernel_m<3" $((2 * (12*4096*(960+320*2) + 320*960*9))) python3 tools/conv_only.py 12 960 64 320 5 &&
+  VP2P_K10_PLAN=0,1 run g960 "conv_kernel_g<3" $((2 * (12*4096*(960+320*2) + 320*960*9))) python3 tools/conv_only.py 12 960 64 320 5 &&
+  echo all-ok
+  exit $?
+fi
 mkdir -p $out/c3 $out/c3r32 $out/sres $out/splain $out/sgeglu
 # algorithmic bytes: x + W + residual in, y out (bf16)
 run c3 "conv_kernel_w<3" $((2 * (32*4096*320*3 + 320*320*9))) python3 tools/conv_only.py 32 320 64 320 5 &&
